@@ -1,0 +1,144 @@
+"""Writes tests/golden/reference_vectors.json.
+
+Every expected value below is TRANSCRIBED, not computed: each case cites where
+its expected output was observed --
+  * "RFC6455-5.7": the known-answer frames printed in RFC 6455 section 5.7;
+  * "SURVEY-a-N": an output of the reference's own src/ws/WSHandler.cpp, run
+    in the survey container and recorded in SURVEY.md section 8 (row a-N).
+Nothing here imports or runs the oracle or the product, so the JSON pins the
+oracle (tests/test_oracle_golden.py) instead of echoing it.
+
+Large payloads are described by a generator name + length instead of bytes:
+  "zeros"  -> b"\\0" * n,   "iota" -> bytes(i & 0xFF for i in range(n)).
+"""
+import json
+import os
+
+HELLO = "48656c6c6f"
+MASKED_HELLO = "37fa213d" + "7f9f4d5158"  # RFC 6455 5.7: key 37 fa 21 3d, masked "Hello"
+
+
+def frame(fin=1, rsv1=0, rsv2=0, rsv3=0, opcode=2, mask=0, length=0, maskey="00000000",
+          payload_hex=None, payload_gen=None):
+    f = dict(fin=fin, rsv1=rsv1, rsv2=rsv2, rsv3=rsv3, opcode=opcode, mask=mask,
+             length=length, maskey=maskey)
+    if payload_hex is not None:
+        f["payload_hex"] = payload_hex
+    else:
+        f["payload_gen"] = payload_gen
+    return f
+
+
+CLIENT, SERVER = "CLIENT", "SERVER"
+
+decode = []
+
+
+def D(name, src, mode, input_hex, rets, frames, chunk=0, tail_gen=None, tail_len=0, then=None):
+    c = dict(name=name, source=src, mode=mode, input_hex=input_hex, chunk=chunk,
+             expect_rets=rets, expect_frames=frames)
+    if tail_gen:
+        c["tail_gen"], c["tail_len"] = tail_gen, tail_len
+    if then:
+        c["then"] = then  # list of {input_hex, expect_rets} fed afterwards to the same decoder
+    decode.append(c)
+
+
+# --- RFC 6455 section 5.7 examples ---------------------------------------------------------
+D("rfc_unmasked_hello", "RFC6455-5.7", CLIENT, "8105" + HELLO, [0],
+  [frame(opcode=1, length=5, payload_hex=HELLO)])
+D("rfc_masked_hello", "RFC6455-5.7; SURVEY-sec4-item2", SERVER, "8185" + MASKED_HELLO, [0],
+  [frame(opcode=1, mask=1, maskey="37fa213d", length=5, payload_hex=HELLO)])
+D("rfc_masked_hello_bytewise", "RFC6455-5.7; SURVEY-a-5 (byte-at-a-time: 1,...,1,0)", SERVER,
+  "8185" + MASKED_HELLO, [1] * 10 + [0],
+  [frame(opcode=1, mask=1, maskey="37fa213d", length=5, payload_hex=HELLO)], chunk=1)
+D("rfc_fragmented_hello", "RFC6455-5.7", CLIENT, "010348656c" + "80026c6f", [0],
+  [frame(fin=0, opcode=1, length=3, payload_hex="48656c"),
+   frame(fin=1, opcode=0, length=2, payload_hex="6c6f")])
+D("rfc_unmasked_ping", "RFC6455-5.7", CLIENT, "8905" + HELLO, [0],
+  [frame(opcode=9, length=5, payload_hex=HELLO)])
+D("rfc_masked_pong", "RFC6455-5.7", SERVER, "8a85" + MASKED_HELLO, [0],
+  [frame(opcode=10, mask=1, maskey="37fa213d", length=5, payload_hex=HELLO)])
+D("rfc_256_binary", "RFC6455-5.7 (header 82 7E 01 00)", CLIENT, "827e0100", [0],
+  [frame(opcode=2, length=256, payload_gen="iota")], tail_gen="iota", tail_len=256)
+D("rfc_64k_binary", "RFC6455-5.7 (header 82 7F 00 00 00 00 00 01 00 00)", CLIENT,
+  "827f0000000000010000", [0],
+  [frame(opcode=2, length=65536, payload_gen="iota")], tail_gen="iota", tail_len=65536)
+
+# --- SURVEY a-5: 127-class extended length quirk (reference run) ---------------------------
+for ext, length in [("0000000100000005", 5), ("0000010000000000", 256),
+                    ("007f000000000000", 8323072), ("0000000000a00000", 10485760)]:
+    D("quirk127_" + ext, "SURVEY-a-5 quirk table", CLIENT, "827f" + ext, [0],
+      [frame(opcode=2, length=length, payload_gen="zeros")], tail_gen="zeros", tail_len=length)
+for ext in ["4000000000000000", "0000000080000000", "0000000000a00001"]:
+    D("quirk127_" + ext, "SURVEY-a-5 quirk table (-> INVALID_LENGTH 6)", CLIENT, "827f" + ext,
+      [6], [])
+
+# --- SURVEY a-5: validation and state rules (reference run) --------------------------------
+D("client_rejects_masked", "SURVEY-a-5 MASKEY: CLIENT + masked -> 7", CLIENT,
+  "8185" + MASKED_HELLO, [7], [])
+D("server_rejects_unmasked", "SURVEY-a-5 MASKEY: SERVER + unmasked + length>0 -> 7", SERVER,
+  "8105" + HELLO, [7], [])
+D("server_accepts_unmasked_empty", "SURVEY-a-5 MASKEY: SERVER + unmasked + length 0 accepted",
+  SERVER, "8100", [0], [frame(opcode=1, length=0, payload_hex="")])
+D("masked_empty_accepted", "SURVEY-a-5 MASKEY: masked length 0 accepted", SERVER,
+  "818001020304", [0], [frame(opcode=1, mask=1, maskey="01020304", length=0, payload_hex="")])
+D("control_not_fin", "SURVEY-a-5 HDR1: !fin && opcode>=8 -> 7", CLIENT, "0900", [7], [])
+D("control_plen_gt_125", "SURVEY-a-5 HDR2: opcode>=8 && plen>125 -> 7", CLIENT, "897e007e",
+  [7], [])
+D("len16_below_126", "SURVEY-a-5 HDREX 126 path: value <126 -> 6", CLIENT, "827e007d", [6], [])
+D("close_stops_parsing", "SURVEY-a-5 DATA: CLOSE delivered, returns 8, trailing bytes unparsed",
+  CLIENT, "880203e8" + "8105" + HELLO, [8], [frame(opcode=8, length=2, payload_hex="03e8")],
+  then=[dict(input_hex="8100", expect_rets=[5])])
+D("error_then_invalid_frame", "SURVEY-a-5: later calls in IN_ERROR -> 5", CLIENT, "0900", [7], [],
+  then=[dict(input_hex="8105" + HELLO, expect_rets=[5])])
+D("empty_input", "SURVEY-a-5 end of input: empty input -> 0", SERVER, "", [0], [])
+D("reserved_opcode_accepted", "SURVEY-a-5 not checked: reserved opcodes 3-7", CLIENT, "830141",
+  [0], [frame(opcode=3, length=1, payload_hex="41")])
+D("rsv_not_checked", "SURVEY-a-5 not checked: RSV bits (checked later, a-14)", CLIENT, "f10141",
+  [0], [frame(rsv1=1, rsv2=1, rsv3=1, opcode=1, length=1, payload_hex="41")])
+D("continuation_order_not_checked", "SURVEY-a-5 not checked: continuation ordering", CLIENT,
+  "800141", [0], [frame(opcode=0, length=1, payload_hex="41")])
+D("partial_header_need_more", "SURVEY-a-5 end of input: non-HDR1 state -> 1", SERVER, "81",
+  [1], [])
+
+# --- SURVEY a-4: encodeFrameHeader outputs (reference run) + RFC headers --------------------
+encode = [
+    dict(name="len65536_masked_rsv1", source="SURVEY-a-4", fin=1, rsv1=1, rsv2=0, rsv3=0,
+         opcode=2, mask=1, maskey="deadbeef", length=65536,
+         expect_hex="c2ff0000000000010000deadbeef"),
+    dict(name="len126_masked_rsv1", source="SURVEY-a-4", fin=1, rsv1=1, rsv2=0, rsv3=0,
+         opcode=2, mask=1, maskey="deadbeef", length=126, expect_hex="c2fe007edeadbeef"),
+    dict(name="rfc_masked_hello_hdr", source="RFC6455-5.7", fin=1, rsv1=0, rsv2=0, rsv3=0,
+         opcode=1, mask=1, maskey="37fa213d", length=5, expect_hex="818537fa213d"),
+    dict(name="rfc_unmasked_hello_hdr", source="RFC6455-5.7", fin=1, rsv1=0, rsv2=0, rsv3=0,
+         opcode=1, mask=0, maskey="00000000", length=5, expect_hex="8105"),
+    dict(name="rfc_fragment1_hdr", source="RFC6455-5.7", fin=0, rsv1=0, rsv2=0, rsv3=0,
+         opcode=1, mask=0, maskey="00000000", length=3, expect_hex="0103"),
+    dict(name="rfc_256_hdr", source="RFC6455-5.7", fin=1, rsv1=0, rsv2=0, rsv3=0, opcode=2,
+         mask=0, maskey="00000000", length=256, expect_hex="827e0100"),
+    dict(name="rfc_64k_hdr", source="RFC6455-5.7", fin=1, rsv1=0, rsv2=0, rsv3=0, opcode=2,
+         mask=0, maskey="00000000", length=65536, expect_hex="827f0000000000010000"),
+]
+
+# --- SURVEY a-2 / a-1: mask vectors (reference run) -----------------------------------------
+mask = [
+    dict(name="chain_3_5", source="SURVEY-a-2 (3-byte + 5-byte chain, key 01 02 03 04)",
+         key="01020304", segments_hex=["000000", "0000000000"],
+         expect_hex=["010203", "0401020304"]),
+    dict(name="rfc_hello", source="RFC6455-5.7", key="37fa213d", segments_hex=[HELLO],
+         expect_hex=["7f9f4d5158"]),
+    dict(name="empty", source="SURVEY-a-1 (len 0 is a no-op)", key="01020304",
+         segments_hex=[""], expect_hex=[""]),
+]
+
+out = dict(
+    about=("Golden vectors for kuma src/ws (WSHandler.cpp). Expected values are transcribed "
+           "from RFC 6455 sec.5.7 and from reference outputs recorded in SURVEY.md sec.8; "
+           "see make_reference_vectors.py."),
+    decode=decode, encode=encode, mask=mask)
+
+path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_vectors.json")
+with open(path, "w") as f:
+    json.dump(out, f, indent=1)
+print("wrote", path, len(decode), "decode,", len(encode), "encode,", len(mask), "mask cases")
