@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident batched WebSocket unmask on MI355X.
+
+Workload (BASELINE.json configs[1], SURVEY.md sec.8 d row 2): per GPU, N frames
+of 64 KiB masked binary payload in an aligned HBM arena (frame i at
+i * 65536) plus 16-byte descriptors {u64 off, u32 len, u32 key}; one step =
+kmws_unmask_batch over the whole batch (plan kernel + unmask kernel), in
+place.  Payload and keys are synthetic (counter-based splitmix64, generated
+on device, untimed).  With --gpus N (torchrun, one rank per GPU) every rank
+unmasks its own batch: a plain per-GPU frame partition (weak scaling), no
+data-path collective; the barrier and the max-over-ranks timing use RCCL.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the formulas.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident WS frame mask/unmask, 64 KiB frames; % HBM peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak, MI355X_MICROARCH.md
+DESC_BYTES = 16
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
+    p.add_argument("--frame-len", type=int, default=65536)
+    p.add_argument("--variant", type=int, default=-1, help="tile variant (-1 = product default)")
+    p.add_argument("--seed", type=int, default=0x6B756D61)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--no-verify", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
+    """Times the oracle (kuma's byte loop, WSHandler.cpp:303-310, restated in
+    oracle/kmws_oracle.c) on host cores over a bounded sample of the same
+    workload: 4096 x frame_len frames, repeated for ~`seconds`."""
+    import numpy as np
+    from oracle import oracle as orc
+    n = 4096
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, size=n * frame_len, dtype=np.uint8)
+    descs = np.zeros(n, dtype=orc.DESC_DTYPE)
+    descs["off"] = np.arange(n, dtype=np.uint64) * frame_len
+    descs["len"] = frame_len
+    descs["key"] = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    orc.unmask_batch(base, descs, threads)  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        orc.unmask_batch(base, descs, threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gib = passes * n * frame_len / 2**30
+    return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x {frame_len} B frames ({n * frame_len >> 20} MiB), in-place unmask with the "
+                      f"oracle's restatement of WSHandler::handleDataMask (scalar byte loop, gcc -O3), "
+                      f"{threads} threads, {passes} passes in {el:.1f} s",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def traffic_from_profile(frames: int, frame_len: int):
+    """HBM bytes per launch of the unmask kernel from the committed PMC pass
+    (profiles/*_traffic.json, written by tools/pmc_traffic.py), if it was
+    measured on this exact configuration; else None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("frames") == frames and t.get("frame_len") == frame_len:
+            best = t
+    return None if best is None else best.get("hbm_bytes_per_launch")
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from kuma_amd import kmws
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if kmws.device_count() < 1:
+        raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
+
+    n, L = a.frames, a.frame_len
+    span = n * L
+    seed = a.seed + rank * 0x1000003  # each rank owns a distinct shard
+    key_seed = seed ^ 0x5EED
+    base = torch.empty(span, dtype=torch.uint8, device=dev)
+    descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span), device=dev)
+    kmws.fill_synthetic(base, seed)
+    kmws.fill_uniform_descs(descs, L, L, key_seed)
+    torch.cuda.synchronize()
+
+    variant = None if a.variant < 0 else a.variant
+    stream = torch.cuda.current_stream()
+
+    def step(ev0=None, ev1=None):
+        if variant is None:
+            kmws.unmask_plan(descs, ws, span)
+            if ev0 is not None:
+                ev0.record(stream)
+            kmws.unmask_apply(base, descs, ws, span)
+            if ev1 is not None:
+                ev1.record(stream)
+        else:
+            if ev0 is not None:
+                ev0.record(stream)
+            kmws.unmask_batch(base, descs, ws, span, variant=variant)
+            if ev1 is not None:
+                ev1.record(stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(*evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    st = ws.status()
+    mismatches = None
+    if not a.no_verify:
+        applied = a.warmup + a.steps
+        if applied % 2 == 0:  # XOR twice is the identity: bring the arena to the unmasked state
+            kmws.unmask_batch(base, descs, ws, span)
+        mismatches = kmws.check_unmasked(base, seed, descs)
+        if world > 1:
+            t = torch.tensor([mismatches], dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            mismatches = int(t[0])
+
+    ms_per_step = elapsed * 1e3 / a.steps
+    total_payload = world * span
+    value = total_payload / (elapsed / a.steps) / 2**30
+    alg_bytes = n * (2 * L + DESC_BYTES)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = traffic_from_profile(n, L)
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if a.cpu_seconds > 0 and world == 1:
+            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(a.cpu_seconds, thr, L, a.seed)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (device-generated splitmix64 payload, per-frame random keys)",
+            "config": {"workload": "cfg2: 1 GPU device-resident in-place unmask of masked binary frames "
+                                   "(aligned arena); N GPUs = per-GPU frame partition",
+                       "frames_per_gpu": n, "frame_len": L, "total_frames": n * world,
+                       "layout": "aligned arena, frame i at i*frame_len",
+                       "parallelism": f"frame-partition x{world} (no collective)",
+                       "tile_variant": "default" if variant is None else variant},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "unmask_tiles_kernel", "kernel_ms": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /
+                                         (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "verify": {"status_word": st, "byte_mismatches": mismatches},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if st != 0 or (mismatches not in (None, 0)):
+        raise SystemExit(f"bench: verification failed (status={st}, mismatches={mismatches})")
+
+
+if __name__ == "__main__":
+    main()

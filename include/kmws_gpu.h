@@ -1,0 +1,171 @@
+/*
+ * kmws_gpu.h -- C ABI of the MI355X (gfx950) WebSocket frame codec.
+ *
+ * Drop-in boundary for kuma's RFC 6455 codec (reference: src/ws/WSHandler.h:32-91,
+ * used by WebSocket::Impl, src/ws/WebSocketImpl.cpp).  Plain C: fixed-width
+ * integers, raw pointers and sizes; a HIP stream is passed as `void*`
+ * (a hipStream_t, NULL = the default stream).  Every function returns a
+ * kmws_status (0 = OK, negative = kuma KMError value, include/kmdefs.h:61-86)
+ * unless noted; codec results use kuma's WSError numbering (wsdefs.h:56-67).
+ *
+ * Two families:
+ *  - host codec entries (kmws_encode_header, kmws_decoder_*): the per-connection,
+ *    byte-stream state machine that kuma runs on its event-loop thread.  The
+ *    decoder parses headers on the host; payload unmasking is done by the GPU
+ *    kernels below (batched per feed call).  See DESIGN.md "Boundary".
+ *  - device batch entries (kmws_*_batch): stream-ordered, no host sync, no
+ *    allocation; all pointers are device pointers; workspace is caller-owned.
+ */
+#ifndef KMWS_GPU_H
+#define KMWS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: kuma KMError values (include/kmdefs.h:61-86) ---- */
+typedef int kmws_status;
+#define KMWS_OK                    0
+#define KMWS_ERR_FAILED           (-1)   /* KMError::FAILED (HIP runtime error) */
+#define KMWS_ERR_INVALID_STATE    (-7)   /* KMError::INVALID_STATE */
+#define KMWS_ERR_INVALID_PARAM    (-8)   /* KMError::INVALID_PARAM */
+#define KMWS_ERR_BUFFER_TOO_SMALL (-17)  /* KMError::BUFFER_TOO_SMALL */
+#define KMWS_ERR_NOT_SUPPORTED    (-19)  /* KMError::NOT_SUPPORTED (no gfx950 device) */
+
+/* ---- codec results: WSError (src/ws/wsdefs.h:56-67) ---- */
+enum kmws_ws_error {
+    KMWS_WS_NOERR = 0, KMWS_WS_NEED_MORE_DATA = 1, KMWS_WS_HANDSHAKE = 2,
+    KMWS_WS_INVALID_PARAM = 3, KMWS_WS_INVALID_STATE = 4, KMWS_WS_INVALID_FRAME = 5,
+    KMWS_WS_INVALID_LENGTH = 6, KMWS_WS_PROTOCOL_ERROR = 7, KMWS_WS_CLOSED = 8,
+    KMWS_WS_DESTROYED = 9
+};
+
+/* WSMode (wsdefs.h:69-72) */
+enum kmws_mode { KMWS_MODE_CLIENT = 0, KMWS_MODE_SERVER = 1 };
+
+/* WSOpcode (wsdefs.h:47-54) */
+enum kmws_opcode { KMWS_OP_CONTINUE = 0, KMWS_OP_TEXT = 1, KMWS_OP_BINARY = 2,
+                   KMWS_OP_CLOSE = 8, KMWS_OP_PING = 9, KMWS_OP_PONG = 10 };
+
+#define KMWS_MASK_KEY_SIZE   4          /* WS_MASK_KEY_SIZE, wsdefs.h:36 */
+#define KMWS_MAX_HEADER_SIZE 14         /* WS_MAX_HEADER_SIZE, wsdefs.h:37 */
+#define KMWS_MAX_FRAME_DATA_LENGTH (10u * 1024u * 1024u)  /* WSHandler.cpp:110 */
+
+/* FrameHeader (wsdefs.h:74-88) with the bitfields widened to bytes. */
+typedef struct kmws_frame_hdr {
+    uint8_t  fin, rsv1, rsv2, rsv3, opcode, mask, plen, reserved;
+    uint64_t xpl64;                      /* union xpl: xpl16 = low 16 bits */
+    uint8_t  maskey[KMWS_MASK_KEY_SIZE]; /* wire order */
+    uint32_t length;
+} kmws_frame_hdr;
+
+/* Frame descriptor in HBM (16 B): payload at base+off, len bytes, key = the
+ * 4 wire key bytes read as a little-endian u32 (== *(uint32_t*)hdr.maskey,
+ * WebSocketImpl.cpp:386). */
+typedef struct kmws_desc {
+    uint64_t off;
+    uint32_t len;
+    uint32_t key;
+} kmws_desc;
+
+/* Per-frame flags for the pack kernels: bits 0-7 = header byte 0
+ * (fin<<7 | rsv1<<6 | rsv2<<5 | rsv3<<4 | opcode), bit 8 = mask. */
+#define KMWS_FLAG_MASK 0x100u
+static inline uint16_t kmws_make_flags(int fin, int rsv1, int rsv2, int rsv3, int opcode, int mask)
+{
+    return (uint16_t)((fin ? 0x80 : 0) | (rsv1 ? 0x40 : 0) | (rsv2 ? 0x20 : 0) |
+                      (rsv3 ? 0x10 : 0) | (opcode & 0x0F) | (mask ? KMWS_FLAG_MASK : 0));
+}
+
+/* ======================= host codec entries ======================= */
+
+/* WSHandler::encodeFrameHeader (WSHandler.cpp:46-106).  Returns the header
+ * length (2, 4 or 10, +4 when masked); out must hold 14 bytes. */
+int kmws_encode_header(const kmws_frame_hdr* hdr, uint8_t out[KMWS_MAX_HEADER_SIZE]);
+
+/* Length of the header kmws_encode_header would write (2/4/10 + 4*mask). */
+int kmws_header_size(uint32_t length, int mask);
+
+/* ---- streaming decoder: WSHandler (WSHandler.h:32-91) ---- */
+typedef struct kmws_decoder kmws_decoder;
+
+/* Frame callback: WSHandler::FrameCallback (WSHandler.h:35).  The payload
+ * view is valid only during the call (WSHandler.cpp:285).  Return nonzero if
+ * the callback destroyed the owner; the decoder then returns
+ * KMWS_WS_DESTROYED without touching itself (DESTROY_DETECTOR, :284-287). */
+typedef int (*kmws_frame_cb)(const kmws_frame_hdr* hdr, uint8_t* payload, size_t len, void* user);
+
+/* mode: kmws_mode.  device: HIP device used for payload unmasking. */
+kmws_decoder* kmws_decoder_create(int mode, int device);
+void          kmws_decoder_destroy(kmws_decoder* dec);
+void          kmws_decoder_set_mode(kmws_decoder* dec, int mode);   /* WSHandler::setMode */
+void          kmws_decoder_reset(kmws_decoder* dec);                /* WSHandler::reset, :324-327 */
+
+/* WSHandler::handleData (WSHandler.cpp:41-44 -> decodeFrame :108-280).
+ * Same return values and callback sequence; masked payloads are unmasked by
+ * the GPU (one batched launch per call) and, as in kuma, in place in `data`
+ * when a frame lies wholly inside it.  Returns a kmws_ws_error value, or a
+ * negative kmws_status if the GPU step failed. */
+int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_cb cb, void* user);
+
+/* ======================= device batch entries ======================= */
+
+/* Number of HIP devices of arch gfx950 visible (0 => device entries return
+ * KMWS_ERR_NOT_SUPPORTED).  Never falls back to the CPU. */
+int kmws_device_count(void);
+
+/* Workspace bytes needed by kmws_unmask_batch for `span` bytes of payload
+ * address space (tile map + status word). */
+size_t kmws_unmask_workspace_size(uint64_t span);
+
+/* Batched in-place unmask (replaces WSHandler::handleDataMask, WSHandler.cpp:
+ * 291-310, for a whole batch).  Frame i's bytes base[off .. off+len) are XORed
+ * with key byte (j % 4) for payload position j.  Preconditions: descs sorted
+ * by off, non-overlapping, off+len <= span; base 16-byte aligned.  The kernel
+ * rewrites whole 16-byte words of each frame's aligned hull (bytes outside a
+ * payload keep their value); nothing may write those hull bytes concurrently.
+ * A precondition violation sets the workspace status word (kmws_read_status)
+ * and leaves the payload untouched. */
+kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+/* kmws_unmask_batch in two stream-ordered halves: `plan` validates the
+ * descriptors and builds the tile map in the workspace; `apply` runs the
+ * unmask kernel.  A plan stays valid for the same (descs, n, span). */
+kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
+                             size_t workspace_bytes, void* stream);
+kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                              const void* workspace, size_t workspace_bytes, void* stream);
+
+/* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2). */
+kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                      void* workspace, size_t workspace_bytes, void* stream, int variant);
+
+/* Read (synchronously) the status word of a workspace after a batch call:
+ * 0 = OK, 1 = descriptor precondition violated, 2 = header error seen. */
+kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream);
+
+/* ---- synthetic data + checks (bench / test support, device side) ---- */
+
+/* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */
+kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream);
+
+/* Uniform descriptors: desc i = {i*stride, len, key_i}, key_i = low 32 bits of
+ * splitmix64(key_seed + i). */
+kmws_status kmws_fill_uniform_descs(kmws_desc* descs, uint32_t n, uint64_t stride, uint32_t len,
+                                    uint64_t key_seed, void* stream);
+
+/* Independent byte-wise checker: counts bytes of base[0..bytes) that differ
+ * from synthetic(seed) XOR (the key byte of the covering frame, if any) into
+ * *mismatches (device u64, accumulated).  Descriptors must be sorted. */
+kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t seed,
+                                const kmws_desc* descs, uint32_t n,
+                                unsigned long long* mismatches, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMWS_GPU_H */

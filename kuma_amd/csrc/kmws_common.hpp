@@ -1,0 +1,57 @@
+// Shared device helpers for the kmws kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "kmws_gpu.h"
+
+namespace kmws {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;          // 4 waves of 64 lanes
+
+// First 16 bytes of every workspace: status word (+ pad), zeroed by a
+// hipMemsetAsync at the start of each batch call.
+struct WsHead {
+    uint32_t status;
+    uint32_t pad[3];
+};
+constexpr uint32_t kStatusBadDesc = 1u;
+constexpr uint32_t kStatusBadHeader = 2u;
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Mask word for an aligned dword whose first byte sits at (address - frame
+// start) == -o (mod 4): byte j of the dword takes key byte (j - o) & 3, i.e.
+// rotl32(key, 8*(o & 3)) with key = LE u32 of the wire key bytes.
+__device__ __forceinline__ uint32_t rot_key(uint32_t key, uint64_t frame_off)
+{
+    return __builtin_rotateleft32(key, (uint32_t)(frame_off & 3u) * 8u);
+}
+
+// Byte-select mask for bytes [lo, hi) of dword d (0..3) of a 16-byte word.
+__device__ __forceinline__ uint32_t dword_byte_mask(int lo, int hi, int d)
+{
+    int a = lo - 4 * d, b = hi - 4 * d;
+    a = a < 0 ? 0 : a;
+    b = b > 4 ? 4 : b;
+    if (b <= a) return 0u;
+    uint32_t hm = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    uint32_t lm = (1u << (8 * a)) - 1u;
+    return hm & ~lm;
+}
+
+inline kmws_status hip_status(hipError_t e)
+{
+    return e == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
+}
+
+}  // namespace kmws

@@ -1,0 +1,383 @@
+// Batched in-place WebSocket payload unmask for MI355X (gfx950).
+//
+// Replaces the per-frame scalar loop WSHandler::handleDataMask
+// (src/ws/WSHandler.cpp:303-310; gate :291-301) with one stream-ordered pass
+// over a whole descriptor batch.  Byte semantics are identical: payload byte
+// j of a frame is XORed with maskey[j % 4]; key phase restarts per frame.
+//
+// Layout: the payload address space [0, span) of `base` is cut into fixed
+// tiles of kTile bytes.  A prep kernel writes, for every tile, the index of
+// the frame whose region (its offset up to the next frame's offset) contains
+// the tile start, so a tile block finds its frames with one load.  The main
+// kernel block (256 lanes) issues its 16-byte loads first, then stages the
+// descriptors of the frames overlapping its tile in LDS and builds a per-word
+// mask (a rotated key splatted over the payload bytes of the word; header or
+// gap bytes get 0), XORs and stores whole 16-byte words.  HBM-bound: 2 bytes
+// of traffic per payload byte + 16 B per descriptor; no MFMA.
+#include "kmws_common.hpp"
+
+namespace kmws {
+
+// Each lane owns V consecutive-block words: word w = tid + kBlock * i.
+template <int V>
+struct UnmaskCfg {
+    static constexpr int kWords = kBlock * V;
+    static constexpr uint64_t kTile = (uint64_t)kWords * 16u;
+    static constexpr int kCap = kBlock;  // descriptors staged per LDS round
+};
+
+// Tile -> first frame map.  Frame f owns tile starts in [start_f, next_f)
+// where start_0 = 0, start_f = off_f, next_f = off_{f+1} (span for the last).
+// Validates sortedness / non-overlap / bounds on the fly.
+__global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __restrict__ d, uint32_t n,
+                                                          uint64_t span, uint32_t tile_shift,
+                                                          uint32_t* __restrict__ map,
+                                                          WsHead* __restrict__ head)
+{
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n) return;
+    const kmws_desc df = d[f];
+    const uint64_t next = (f + 1 < n) ? d[f + 1].off : span;
+    if (df.off > span || df.off + (uint64_t)df.len > next) {
+        atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    const uint64_t start = f == 0 ? 0 : df.off;
+    const uint64_t T = 1ull << tile_shift;
+    const uint64_t b0 = (start + T - 1) >> tile_shift;
+    const uint64_t b1 = (next + T - 1) >> tile_shift;
+    for (uint64_t b = b0; b < b1; ++b) map[b] = f;
+}
+
+template <int V, bool FULL>
+__device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
+                                            const kmws_desc* __restrict__ d, uint32_t n, uint32_t f,
+                                            uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
+{
+    using Cfg = UnmaskCfg<V>;
+    const int tid = threadIdx.x;
+
+    // 1) Issue every payload load of this lane before any metadata work.
+    //    Full tiles load unconditionally so the loads stay back to back.
+    u32x4 v[V];
+    u32x4 m[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
+        if (FULL || a < tile_hi) v[i] = *reinterpret_cast<const u32x4*>(base + a);
+        else v[i] = u32x4{0, 0, 0, 0};
+        m[i] = u32x4{0, 0, 0, 0};
+    }
+
+    // 2) Stage the descriptors of frames overlapping the tile, kCap per round.
+    for (;;) {
+        const uint32_t fi = f + (uint32_t)tid;
+        int valid = 0;
+        if (fi < n) {
+            const u32x4 x = *reinterpret_cast<const u32x4*>(d + fi);  // one 16-B load
+            const uint64_t off = (uint64_t)x.x | ((uint64_t)x.y << 32);
+            if (off < tile_hi) {
+                valid = 1;
+                s_off[tid] = off;
+                s_end[tid] = off + x.z;
+                s_key[tid] = x.w;
+            }
+        }
+        const int cnt = __syncthreads_count(valid);  // sorted => a prefix
+
+        // 3) Per-word mask from the staged frames.
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
+            int lo = 0, hi = cnt;  // first staged frame with end > a
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_end[mid] <= a) lo = mid + 1; else hi = mid;
+            }
+            for (int j = lo; j < cnt; ++j) {
+                const uint64_t o = s_off[j];
+                if (o >= a + 16) break;
+                const uint64_t e = s_end[j];
+                const uint32_t r = rot_key(s_key[j], o);
+                if (o <= a && e >= a + 16) {
+                    m[i] |= u32x4{r, r, r, r};
+                } else {
+                    const int blo = o > a ? (int)(o - a) : 0;
+                    const int bhi = e < a + 16 ? (int)(e - a) : 16;
+                    m[i].x |= r & dword_byte_mask(blo, bhi, 0);
+                    m[i].y |= r & dword_byte_mask(blo, bhi, 1);
+                    m[i].z |= r & dword_byte_mask(blo, bhi, 2);
+                    m[i].w |= r & dword_byte_mask(blo, bhi, 3);
+                }
+            }
+        }
+        if (cnt < Cfg::kCap) break;
+        f += Cfg::kCap;
+        __syncthreads();  // every lane done reading this round's LDS
+    }
+
+    // 4) XOR and store the words that carry payload bytes.
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
+        const u32x4 mm = m[i];
+        if ((FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
+            *reinterpret_cast<u32x4*>(base + a) = v[i] ^ mm;
+    }
+}
+
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
+                                                              const kmws_desc* __restrict__ d, uint32_t n,
+                                                              const uint32_t* __restrict__ map,
+                                                              const WsHead* __restrict__ head)
+{
+    using Cfg = UnmaskCfg<V>;
+    __shared__ uint64_t s_off[Cfg::kCap];
+    __shared__ uint64_t s_end[Cfg::kCap];
+    __shared__ uint32_t s_key[Cfg::kCap];
+
+    if (head->status != 0) return;  // prep found a bad descriptor: touch nothing
+    const uint64_t tile_lo = (uint64_t)blockIdx.x * Cfg::kTile;
+    const uint32_t f = map[blockIdx.x];
+    if (tile_lo + Cfg::kTile <= span)
+        unmask_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, f, s_off, s_end, s_key);
+    else
+        unmask_tile<V, false>(base, tile_lo, span, d, n, f, s_off, s_end, s_key);
+}
+
+// ---- synthetic fill: byte i = byte (i & 7) of splitmix64(seed + (i >> 3)) ----
+__global__ void __launch_bounds__(kBlock) fill_synthetic_kernel(uint8_t* __restrict__ base, uint64_t bytes,
+                                                                uint64_t seed)
+{
+    const uint64_t nw = bytes >> 4;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x; w < nw; w += stride) {
+        const uint64_t a = splitmix64(seed + 2 * w), b = splitmix64(seed + 2 * w + 1);
+        *reinterpret_cast<u32x4*>(base + 16 * w) =
+            u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) {
+        const uint64_t i = (nw << 4) + threadIdx.x;
+        base[i] = (uint8_t)(splitmix64(seed + (i >> 3)) >> (8 * (i & 7)));
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) uniform_descs_kernel(kmws_desc* __restrict__ d, uint32_t n,
+                                                               uint64_t stride, uint32_t len, uint64_t key_seed)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    kmws_desc x;
+    x.off = (uint64_t)i * stride;
+    x.len = len;
+    x.key = (uint32_t)splitmix64(key_seed + i);
+    d[i] = x;
+}
+
+// ---- independent checker: simple byte-wise restatement, not the product path ----
+constexpr int kCheckBytes = 4096;  // bytes per checker block
+
+__global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* __restrict__ base, uint64_t bytes,
+                                                                uint64_t seed, const kmws_desc* __restrict__ d,
+                                                                uint32_t n, unsigned long long* mismatches)
+{
+    __shared__ uint32_t s_first;
+    const uint64_t blk_lo = (uint64_t)blockIdx.x * kCheckBytes;
+    if (threadIdx.x == 0) {
+        // first frame with off + len > blk_lo (binary search over sorted descs)
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (d[mid].off + d[mid].len <= blk_lo) lo = mid + 1; else hi = mid;
+        }
+        s_first = lo;
+    }
+    __syncthreads();
+    uint32_t f = s_first;
+    unsigned long long bad = 0;
+    const uint64_t p0 = blk_lo + 16u * threadIdx.x;
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t p = p0 + k;
+        if (p >= bytes) break;
+        while (f < n && d[f].off + d[f].len <= p) ++f;
+        uint8_t expect = (uint8_t)(splitmix64(seed + (p >> 3)) >> (8 * (p & 7)));
+        if (f < n && d[f].off <= p) {
+            const uint32_t key = d[f].key;
+            expect ^= (uint8_t)(key >> (8 * ((p - d[f].off) & 3)));
+        }
+        bad += base[p] != expect;
+    }
+    if (bad) atomicAdd(mismatches, bad);
+}
+
+// Tile geometry used by the product path (tuned on MI355X).
+constexpr int kUnmaskV = 4;
+using ProdCfg = UnmaskCfg<kUnmaskV>;
+
+static uint32_t ilog2_u64(uint64_t x)
+{
+    uint32_t r = 0;
+    while ((1ull << r) < x) ++r;
+    return r;
+}
+
+template <int V>
+static kmws_status check_ws(uint64_t span, size_t ws_bytes, uint64_t* ntiles_out)
+{
+    using Cfg = UnmaskCfg<V>;
+    const uint64_t ntiles = (span + Cfg::kTile - 1) / Cfg::kTile;
+    if (ntiles > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    if (ws_bytes < sizeof(WsHead) + ntiles * sizeof(uint32_t)) return KMWS_ERR_BUFFER_TOO_SMALL;
+    *ntiles_out = ntiles;
+    return KMWS_OK;
+}
+
+template <int V>
+static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
+                               size_t ws_bytes, hipStream_t s)
+{
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    WsHead* head = static_cast<WsHead*>(workspace);
+    if (hipMemsetAsync(head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
+    if (n == 0 || span == 0) return KMWS_OK;
+    hipLaunchKernelGGL(tile_map_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, n, span,
+                       ilog2_u64(UnmaskCfg<V>::kTile), reinterpret_cast<uint32_t*>(head + 1), head);
+    return hip_status(hipGetLastError());
+}
+
+template <int V>
+static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                const void* workspace, size_t ws_bytes, hipStream_t s)
+{
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    if (n == 0 || span == 0) return KMWS_OK;
+    const WsHead* head = static_cast<const WsHead*>(workspace);
+    hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3((uint32_t)ntiles), dim3(kBlock), 0, s, base, span, descs, n,
+                       reinterpret_cast<const uint32_t*>(head + 1), head);
+    return hip_status(hipGetLastError());
+}
+
+template <int V>
+static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                 void* workspace, size_t ws_bytes, hipStream_t s)
+{
+    kmws_status st = launch_plan<V>(span, descs, n, workspace, ws_bytes, s);
+    if (st != KMWS_OK) return st;
+    return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
+}
+
+static bool bad_args(const uint8_t* base, const kmws_desc* descs, uint32_t n, const void* ws)
+{
+    return !ws || (n && (!base || !descs)) || (reinterpret_cast<uintptr_t>(base) & 15u);
+}
+
+}  // namespace kmws
+
+using namespace kmws;
+
+extern "C" {
+
+size_t kmws_unmask_workspace_size(uint64_t span)
+{
+    // sized for the smallest tile any variant uses
+    const uint64_t ntiles = (span + UnmaskCfg<4>::kTile - 1) / UnmaskCfg<4>::kTile;
+    return sizeof(WsHead) + (size_t)ntiles * sizeof(uint32_t);
+}
+
+kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                              void* workspace, size_t workspace_bytes, void* stream)
+{
+    if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
+    return launch_unmask<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes,
+                                   static_cast<hipStream_t>(stream));
+}
+
+kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
+                             size_t workspace_bytes, void* stream)
+{
+    if (!workspace || (n && !descs)) return KMWS_ERR_INVALID_PARAM;
+    return launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+}
+
+kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                              const void* workspace, size_t workspace_bytes, void* stream)
+{
+    if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
+    return launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes,
+                                  static_cast<hipStream_t>(stream));
+}
+
+// Tuning entry: same contract as kmws_unmask_batch with an explicit tile
+// variant (0: 16 KiB, 1: 32 KiB, 2: 64 KiB).  Used by bench/tune scripts.
+kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                      void* workspace, size_t workspace_bytes, void* stream, int variant)
+{
+    if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (variant) {
+    case 0: return launch_unmask<4>(base, span, descs, n, workspace, workspace_bytes, s);
+    case 1: return launch_unmask<8>(base, span, descs, n, workspace, workspace_bytes, s);
+    case 2: return launch_unmask<16>(base, span, descs, n, workspace, workspace_bytes, s);
+    default: return KMWS_ERR_INVALID_PARAM;
+    }
+}
+
+kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream)
+{
+    if (!workspace || !status_out) return KMWS_ERR_INVALID_PARAM;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemcpyAsync(status_out, workspace, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return hip_status(e);
+}
+
+kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream)
+{
+    if (!base && bytes) return KMWS_ERR_INVALID_PARAM;
+    if ((reinterpret_cast<uintptr_t>(base) & 15u)) return KMWS_ERR_INVALID_PARAM;
+    if (bytes == 0) return KMWS_OK;
+    hipLaunchKernelGGL(fill_synthetic_kernel, dim3(8192), dim3(kBlock), 0, static_cast<hipStream_t>(stream), base,
+                       bytes, seed);
+    return hip_status(hipGetLastError());
+}
+
+kmws_status kmws_fill_uniform_descs(kmws_desc* descs, uint32_t n, uint64_t stride, uint32_t len,
+                                    uint64_t key_seed, void* stream)
+{
+    if (!descs && n) return KMWS_ERR_INVALID_PARAM;
+    if (n == 0) return KMWS_OK;
+    hipLaunchKernelGGL(uniform_descs_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), descs, n, stride, len, key_seed);
+    return hip_status(hipGetLastError());
+}
+
+kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t seed, const kmws_desc* descs,
+                                uint32_t n, unsigned long long* mismatches, void* stream)
+{
+    if ((!base && bytes) || !mismatches) return KMWS_ERR_INVALID_PARAM;
+    if (bytes == 0) return KMWS_OK;
+    const uint64_t nb = (bytes + kCheckBytes - 1) / kCheckBytes;
+    if (nb > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    hipLaunchKernelGGL(check_unmasked_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       base, bytes, seed, descs, n, mismatches);
+    return hip_status(hipGetLastError());
+}
+
+int kmws_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    return good;
+}
+
+}  // extern "C"

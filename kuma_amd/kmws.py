@@ -1,0 +1,288 @@
+"""ctypes binding of the kmws C ABI (include/kmws_gpu.h).
+
+Mirrors the reference codec interface (kuma::ws::WSHandler, src/ws/WSHandler.h:
+32-91) for Python callers and tests, and exposes the device batch entries over
+torch tensors (torch is plumbing here: device memory and streams).  There is no
+CPU fallback anywhere in this module: if libkmws_gpu.so is missing the import
+fails, and device entries on a machine without a gfx950 GPU return
+KMWS_ERR_NOT_SUPPORTED.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+from . import build as _build
+
+# ---- constants (include/kmws_gpu.h) ----
+OK, ERR_FAILED, ERR_INVALID_STATE, ERR_INVALID_PARAM = 0, -1, -7, -8
+ERR_BUFFER_TOO_SMALL, ERR_NOT_SUPPORTED = -17, -19
+CLIENT, SERVER = 0, 1
+OP_CONTINUE, OP_TEXT, OP_BINARY, OP_CLOSE, OP_PING, OP_PONG = 0, 1, 2, 8, 9, 10
+WS_NOERR, WS_NEED_MORE_DATA, WS_INVALID_FRAME, WS_INVALID_LENGTH = 0, 1, 5, 6
+WS_PROTOCOL_ERROR, WS_CLOSED, WS_DESTROYED = 7, 8, 9
+MAX_HEADER_SIZE = 14
+FLAG_MASK = 0x100
+
+#: every function include/kmws_gpu.h declares (tests check they are exported)
+EXPORTS = [
+    "kmws_encode_header", "kmws_header_size", "kmws_decoder_create", "kmws_decoder_destroy",
+    "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
+    "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
+    "kmws_unmask_batch_variant", "kmws_read_status", "kmws_fill_synthetic",
+    "kmws_fill_uniform_descs", "kmws_check_unmasked",
+]
+
+
+class FrameHdr(C.Structure):
+    """kmws_frame_hdr == FrameHeader (src/ws/wsdefs.h:74-88), bitfields widened."""
+    _fields_ = [("fin", C.c_uint8), ("rsv1", C.c_uint8), ("rsv2", C.c_uint8), ("rsv3", C.c_uint8),
+                ("opcode", C.c_uint8), ("mask", C.c_uint8), ("plen", C.c_uint8),
+                ("reserved", C.c_uint8), ("xpl64", C.c_uint64), ("maskey", C.c_uint8 * 4),
+                ("length", C.c_uint32)]
+
+
+FRAME_CB = C.CFUNCTYPE(C.c_int, C.POINTER(FrameHdr), C.POINTER(C.c_uint8), C.c_size_t, C.c_void_p)
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def lib() -> C.CDLL:
+    """Load libkmws_gpu.so (building it first when hipcc is available)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not _build.up_to_date():
+        try:
+            _build.build()
+        except (OSError, Exception) as e:  # no hipcc on this machine: use the shipped .so
+            if not os.path.exists(path):
+                raise RuntimeError(f"kmws: {path} missing and cannot be built: {e}") from e
+    if not os.path.exists(path):
+        raise RuntimeError(f"kmws: HIP library {path} not built (run __graft_entry__.build())")
+    L = C.CDLL(path)
+    vp, u8p, sz, u32, u64, i32 = C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
+    sig = {
+        "kmws_encode_header": (i32, [C.POINTER(FrameHdr), u8p]),
+        "kmws_header_size": (i32, [u32, i32]),
+        "kmws_decoder_create": (vp, [i32, i32]),
+        "kmws_decoder_destroy": (None, [vp]),
+        "kmws_decoder_set_mode": (None, [vp, i32]),
+        "kmws_decoder_reset": (None, [vp]),
+        "kmws_decoder_feed": (i32, [vp, u8p, sz, FRAME_CB, vp]),
+        "kmws_device_count": (i32, []),
+        "kmws_unmask_workspace_size": (sz, [u64]),
+        "kmws_unmask_batch": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
+        "kmws_unmask_plan": (i32, [u64, vp, u32, vp, sz, vp]),
+        "kmws_unmask_apply": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
+        "kmws_unmask_batch_variant": (i32, [u8p, u64, vp, u32, vp, sz, vp, i32]),
+        "kmws_read_status": (i32, [vp, C.POINTER(C.c_uint32), vp]),
+        "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
+        "kmws_fill_uniform_descs": (i32, [vp, u32, u64, u32, u64, vp]),
+        "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = L
+    return L
+
+
+def _check(st: int, what: str) -> None:
+    if st != OK:
+        raise RuntimeError(f"{what} failed with kmws_status {st}")
+
+
+# ====================== host codec (WSHandler mirror) ======================
+
+@dataclass
+class Header:
+    fin: int = 1
+    rsv1: int = 0
+    rsv2: int = 0
+    rsv3: int = 0
+    opcode: int = OP_BINARY
+    mask: int = 0
+    maskey: bytes = b"\0\0\0\0"
+    length: int = 0
+    plen: int = 0
+    xpl64: int = 0
+
+    def to_c(self) -> FrameHdr:
+        h = FrameHdr()
+        h.fin, h.rsv1, h.rsv2, h.rsv3 = self.fin, self.rsv1, self.rsv2, self.rsv3
+        h.opcode, h.mask, h.plen, h.xpl64 = self.opcode, self.mask, self.plen, self.xpl64
+        h.length = self.length & 0xFFFFFFFF
+        for i in range(4):
+            h.maskey[i] = self.maskey[i]
+        return h
+
+    @staticmethod
+    def from_c(h: FrameHdr) -> "Header":
+        return Header(h.fin, h.rsv1, h.rsv2, h.rsv3, h.opcode, h.mask, bytes(h.maskey), h.length,
+                      h.plen, h.xpl64)
+
+
+def encode_frame_header(hdr: Header) -> bytes:
+    """WSHandler::encodeFrameHeader (WSHandler.cpp:46-106)."""
+    out = (C.c_uint8 * MAX_HEADER_SIZE)()
+    n = lib().kmws_encode_header(C.byref(hdr.to_c()), out)
+    if n < 0:
+        raise RuntimeError(f"kmws_encode_header: {n}")
+    return bytes(out[:n])
+
+
+def header_size(length: int, mask: bool) -> int:
+    return lib().kmws_header_size(length & 0xFFFFFFFF, int(bool(mask)))
+
+
+class WSHandler:
+    """kuma::ws::WSHandler over the C ABI (WSHandler.h:32-91).
+
+    handleData(data) returns the WSError int and invokes the frame callback
+    `cb(Header, payload: bytes)` for each frame, in order.  Masked payloads are
+    unmasked on the GPU.  If `data` is a bytearray it is unmasked in place like
+    the reference does with the caller's buffer.
+    """
+
+    def __init__(self, mode: int = CLIENT, device: int = 0):
+        self._d = lib().kmws_decoder_create(mode, device)
+        if not self._d:
+            raise MemoryError("kmws_decoder_create")
+        self._cb: Optional[Callable] = None
+        self.destroyed_by_callback = False
+
+        def tramp(hp, payload, n, user):
+            if self._cb is None:
+                return 0
+            data = C.string_at(payload, n) if n else b""
+            r = self._cb(Header.from_c(hp.contents), data)
+            return 1 if r is True else 0
+
+        self._tramp = FRAME_CB(tramp)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_d", None):
+                lib().kmws_decoder_destroy(self._d)
+                self._d = None
+        except Exception:
+            pass
+
+    def setMode(self, mode: int) -> None:
+        lib().kmws_decoder_set_mode(self._d, mode)
+
+    def setFrameCallback(self, cb: Callable) -> None:
+        """cb(Header, bytes) -> optional True to emulate 'callback destroyed the handler'."""
+        self._cb = cb
+
+    def reset(self) -> None:
+        lib().kmws_decoder_reset(self._d)
+
+    def handleData(self, data) -> int:
+        n = len(data)
+        if isinstance(data, bytearray):
+            buf = (C.c_uint8 * max(1, n)).from_buffer(data) if n else (C.c_uint8 * 1)()
+        else:
+            buf = (C.c_uint8 * max(1, n)).from_buffer_copy(bytes(data) if n else b"\0")
+        return lib().kmws_decoder_feed(self._d, buf, n, self._tramp, None)
+
+    encodeFrameHeader = staticmethod(encode_frame_header)
+
+
+# ====================== device batch entries (torch tensors) ======================
+
+def device_count() -> int:
+    return lib().kmws_device_count()
+
+
+def _stream_handle(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def make_descs(off, length, key, device="cuda"):
+    """(n, 2) int64 tensor laid out as kmws_desc {u64 off; u32 len; u32 key}."""
+    import torch
+    off = torch.as_tensor(off, dtype=torch.int64)
+    lk = (torch.as_tensor(length, dtype=torch.int64) & 0xFFFFFFFF) | \
+        (torch.as_tensor(key, dtype=torch.int64) << 32)
+    return torch.stack([off, lk], dim=1).contiguous().to(device)
+
+
+class Workspace:
+    """Caller-owned device workspace (no allocation inside the batch calls)."""
+
+    def __init__(self, nbytes: int, device="cuda"):
+        import torch
+        self.tensor = torch.empty(max(16, int(nbytes)), dtype=torch.uint8, device=device)
+
+    @property
+    def ptr(self) -> int:
+        return self.tensor.data_ptr()
+
+    @property
+    def nbytes(self) -> int:
+        return self.tensor.numel()
+
+    def status(self, stream=None) -> int:
+        out = C.c_uint32(0)
+        _check(lib().kmws_read_status(self.ptr, C.byref(out), _stream_handle(stream)), "kmws_read_status")
+        return out.value
+
+
+def unmask_workspace_size(span: int) -> int:
+    return lib().kmws_unmask_workspace_size(span)
+
+
+def unmask_batch(base, descs, ws: Workspace, span: Optional[int] = None, stream=None,
+                 variant: Optional[int] = None) -> None:
+    """In-place batched unmask (kmws_unmask_batch) of uint8 device tensor `base`."""
+    span = base.numel() if span is None else span
+    n = descs.shape[0]
+    s = _stream_handle(stream)
+    if variant is None:
+        st = lib().kmws_unmask_batch(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr, ws.nbytes, s)
+    else:
+        st = lib().kmws_unmask_batch_variant(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr,
+                                             ws.nbytes, s, variant)
+    _check(st, "kmws_unmask_batch")
+
+
+def unmask_plan(descs, ws: Workspace, span: int, stream=None) -> None:
+    _check(lib().kmws_unmask_plan(span, descs.data_ptr(), descs.shape[0], ws.ptr, ws.nbytes,
+                                  _stream_handle(stream)), "kmws_unmask_plan")
+
+
+def unmask_apply(base, descs, ws: Workspace, span: Optional[int] = None, stream=None) -> None:
+    span = base.numel() if span is None else span
+    _check(lib().kmws_unmask_apply(base.data_ptr(), span, descs.data_ptr(), descs.shape[0], ws.ptr,
+                                   ws.nbytes, _stream_handle(stream)), "kmws_unmask_apply")
+
+
+def fill_synthetic(base, seed: int, nbytes: Optional[int] = None, stream=None) -> None:
+    nbytes = base.numel() if nbytes is None else nbytes
+    _check(lib().kmws_fill_synthetic(base.data_ptr(), nbytes, seed, _stream_handle(stream)),
+           "kmws_fill_synthetic")
+
+
+def fill_uniform_descs(descs, stride: int, length: int, key_seed: int, stream=None) -> None:
+    _check(lib().kmws_fill_uniform_descs(descs.data_ptr(), descs.shape[0], stride, length, key_seed,
+                                         _stream_handle(stream)), "kmws_fill_uniform_descs")
+
+
+def check_unmasked(base, seed: int, descs, nbytes: Optional[int] = None, stream=None) -> int:
+    import torch
+    nbytes = base.numel() if nbytes is None else nbytes
+    cnt = torch.zeros(1, dtype=torch.int64, device=base.device)
+    _check(lib().kmws_check_unmasked(base.data_ptr(), nbytes, seed, descs.data_ptr(), descs.shape[0],
+                                     cnt.data_ptr(), _stream_handle(stream)), "kmws_check_unmasked")
+    return int(cnt.item())

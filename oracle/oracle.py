@@ -171,8 +171,13 @@ class Decoder:
         except Exception:
             pass
 
-    def feed(self, data: bytes) -> int:
-        buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+    def feed(self, data) -> int:
+        """A bytearray is decoded in place (masked payloads unmasked in it, as
+        WSHandler.cpp:247-250/:260 does with the caller's buffer)."""
+        if isinstance(data, bytearray) and len(data):
+            buf = (C.c_uint8 * len(data)).from_buffer(data)
+        else:
+            buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
         return lib().orc_decoder_feed(self._d, buf, len(data), self._cb, None)
 
     def reset(self) -> None:
@@ -196,6 +201,30 @@ def decode_chunks(stream: bytes, mode: int, chunk: int) -> Tuple[List[int], List
         for i in range(0, len(stream), chunk):
             rets.append(d.feed(stream[i:i + chunk]))
     return rets, d.frames
+
+
+def synthetic(seed: int, start: int, nbytes: int) -> np.ndarray:
+    """Host copy of kmws_fill_synthetic: byte i = byte (i & 7) of
+    splitmix64(seed + (i >> 3)), for i in [start, start + nbytes)."""
+    if nbytes <= 0:
+        return np.zeros(0, dtype=np.uint8)
+    w0, w1 = start >> 3, (start + nbytes + 7) >> 3
+    with np.errstate(over="ignore"):
+        z = np.arange(w0, w1, dtype=np.uint64) + np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    s = start - (w0 << 3)
+    return b[s:s + nbytes].copy()
+
+
+def splitmix64(x: int) -> int:
+    M = (1 << 64) - 1
+    z = (x + 0x9E3779B97F4A7C15) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
 
 
 DESC_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("key", "<u4")])

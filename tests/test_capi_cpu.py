@@ -1,0 +1,114 @@
+"""C-ABI checks that need no GPU: the library loads and exports every symbol
+include/kmws_gpu.h declares; host codec entries match the oracle."""
+import os
+import random
+import re
+
+import pytest
+
+from kuma_amd import kmws
+from oracle import oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_decls():
+    txt = open(os.path.join(ROOT, "include", "kmws_gpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = set(re.findall(r"\b(kmws_[a-z0-9_]+)\s*\(", txt))
+    return sorted(n for n in names if n != "kmws_make_flags")  # static inline helper
+
+
+def test_exports_every_declared_symbol():
+    L = kmws.lib()
+    decl = header_decls()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(kmws.EXPORTS) == decl
+
+
+def test_encode_header_matches_oracle():
+    rng = random.Random(7)
+    lens = [0, 1, 2, 124, 125, 126, 127, 65534, 65535, 65536, 65537, 10485760, 2**31, 2**32 - 1]
+    lens += [rng.randrange(2**32) for _ in range(200)]
+    for L in lens:
+        for mask in (0, 1):
+            h = dict(fin=rng.randrange(2), rsv1=rng.randrange(2), rsv2=rng.randrange(2),
+                     rsv3=rng.randrange(2), opcode=rng.randrange(16), mask=mask,
+                     maskey=bytes(rng.randrange(256) for _ in range(4)), length=L)
+            got = kmws.encode_frame_header(kmws.Header(**h))
+            assert got == orc.encode_header(orc.Hdr(**h))
+            assert len(got) == kmws.header_size(L, mask)
+
+
+def _client_stream(rng, nframes):
+    out = b""
+    for _ in range(nframes):
+        n = rng.choice([0, 1, 3, 125, 126, 200, 65535, 65536, 70001])
+        op = rng.choice([0, 1, 2, 3, 9, 10])
+        h = orc.Hdr(fin=1 if op >= 8 else rng.randrange(2), opcode=op, mask=0,
+                    length=min(n, 125) if op >= 8 else n)
+        out += orc.encode_header(h) + bytes(rng.randrange(256) for _ in range(h.length))
+    return out
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 5, 64, 1000, 65536])
+def test_decoder_unmasked_matches_oracle(chunk):
+    """CLIENT-mode streams carry no masked payload, so no device work is needed."""
+    rng = random.Random(100 + chunk)
+    stream = _client_stream(rng, 12 if chunk == 1 else 60)
+    rets_o, frames_o = orc.decode_chunks(stream, orc.CLIENT, chunk)
+    h = kmws.WSHandler(kmws.CLIENT)
+    got = []
+    h.setFrameCallback(lambda hd, p: got.append((hd.fin, hd.rsv1, hd.rsv2, hd.rsv3, hd.opcode, hd.mask,
+                                                 hd.plen, hd.xpl64, hd.maskey, hd.length, p)))
+    rets = []
+    if chunk <= 0:
+        rets.append(h.handleData(stream))
+    else:
+        for i in range(0, len(stream), chunk):
+            rets.append(h.handleData(stream[i:i + chunk]))
+    assert rets == rets_o
+    assert got == [f.key() for f in frames_o]
+
+
+def test_decoder_golden_client_cases():
+    import json
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_vectors.json")))
+    ran = 0
+    for c in gold["decode"]:
+        if c["mode"] != "CLIENT":
+            continue
+        data = bytes.fromhex(c["input_hex"])
+        if "tail_gen" in c:
+            data += bytes(c["tail_len"]) if c["tail_gen"] == "zeros" else \
+                bytes(i & 0xFF for i in range(c["tail_len"]))
+        h = kmws.WSHandler(kmws.CLIENT)
+        frames = []
+        h.setFrameCallback(lambda hd, p: frames.append((hd, p)))
+        step = c["chunk"] or len(data) or 1
+        rets = [h.handleData(data[i:i + step]) for i in range(0, max(1, len(data)), step)]
+        assert rets == c["expect_rets"], c["name"]
+        assert len(frames) == len(c["expect_frames"]), c["name"]
+        for (hd, p), e in zip(frames, c["expect_frames"]):
+            assert (hd.fin, hd.opcode, hd.mask, hd.length) == (e["fin"], e["opcode"], e["mask"], e["length"])
+        for s in c.get("then", []):
+            assert h.handleData(bytes.fromhex(s["input_hex"])) == s["expect_rets"][0]
+        ran += 1
+    assert ran >= 15
+
+
+def test_masked_frame_without_gpu_fails_loudly():
+    if kmws.device_count() > 0:
+        pytest.skip("GPU present")
+    h = kmws.WSHandler(kmws.SERVER)
+    assert h.handleData(bytes.fromhex("818537fa213d7f9f4d5158")) == kmws.ERR_NOT_SUPPORTED
+
+
+def test_synthetic_host_generator():
+    a = orc.synthetic(5, 0, 64)
+    b = orc.synthetic(5, 13, 40)
+    assert (a[13:53] == b).all()
+    w = orc.splitmix64(5 + 1).to_bytes(8, "little")
+    assert bytes(a[8:16]) == w

@@ -1,0 +1,125 @@
+"""GPU parity of the WSHandler-compatible streaming decoder (kmws_decoder_feed,
+whose masked payloads are unmasked by the HIP kernel) against the oracle:
+return codes, callback sequence (every FrameHeader field + payload) and the
+in-place unmask of the caller's buffer."""
+import json
+import os
+import random
+
+import pytest
+
+from kuma_amd import kmws
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_vectors.json")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if kmws.device_count() < 1:
+        pytest.fail("gpu test needs a gfx950 device")
+
+
+def frame_key(hd, p):
+    return (hd.fin, hd.rsv1, hd.rsv2, hd.rsv3, hd.opcode, hd.mask, hd.plen, hd.xpl64, hd.maskey,
+            hd.length, p)
+
+
+def run_kmws(stream, mode, chunk, inplace=False):
+    h = kmws.WSHandler(mode)
+    got = []
+    h.setFrameCallback(lambda hd, p: got.append(frame_key(hd, p)))
+    rets, bufs = [], []
+    step = chunk if chunk > 0 else max(1, len(stream))
+    for i in range(0, max(1, len(stream)), step):
+        piece = bytearray(stream[i:i + step]) if inplace else stream[i:i + step]
+        rets.append(h.handleData(piece))
+        bufs.append(bytes(piece))
+    return rets, got, b"".join(bufs)
+
+
+def run_oracle(stream, mode, chunk, inplace=False):
+    d = orc.Decoder(mode)
+    rets, bufs = [], []
+    step = chunk if chunk > 0 else max(1, len(stream))
+    for i in range(0, max(1, len(stream)), step):
+        piece = bytearray(stream[i:i + step]) if inplace else stream[i:i + step]
+        rets.append(d.feed(piece))
+        bufs.append(bytes(piece))
+    return rets, [f.key() for f in d.frames], b"".join(bufs)
+
+
+@pytest.mark.parametrize("c", GOLD["decode"], ids=lambda c: c["name"])
+def test_golden_through_gpu_decoder(c):
+    data = bytes.fromhex(c["input_hex"])
+    if "tail_gen" in c:
+        data += bytes(c["tail_len"]) if c["tail_gen"] == "zeros" else \
+            bytes(i & 0xFF for i in range(c["tail_len"]))
+    mode = kmws.SERVER if c["mode"] == "SERVER" else kmws.CLIENT
+    h = kmws.WSHandler(mode)
+    frames = []
+    h.setFrameCallback(lambda hd, p: frames.append((hd, p)))
+    step = c["chunk"] or len(data) or 1
+    rets = [h.handleData(data[i:i + step]) for i in range(0, max(1, len(data)), step)]
+    assert rets == c["expect_rets"]
+    assert len(frames) == len(c["expect_frames"])
+    for (hd, p), e in zip(frames, c["expect_frames"]):
+        assert (hd.fin, hd.rsv1, hd.rsv2, hd.rsv3, hd.opcode, hd.mask, hd.length) == \
+            (e["fin"], e["rsv1"], e["rsv2"], e["rsv3"], e["opcode"], e["mask"], e["length"])
+        assert hd.maskey.hex() == e["maskey"]
+        want = bytes.fromhex(e["payload_hex"]) if "payload_hex" in e else (
+            bytes(e["length"]) if e["payload_gen"] == "zeros" else bytes(i & 0xFF for i in range(e["length"])))
+        assert p == want
+    for s in c.get("then", []):
+        assert h.handleData(bytes.fromhex(s["input_hex"])) == s["expect_rets"][0]
+
+
+def masked_stream(seed, nframes, sizes=(0, 1, 3, 4, 5, 125, 126, 127, 1000, 4096, 65535, 65536, 100000)):
+    rng = random.Random(seed)
+    out = b""
+    for _ in range(nframes):
+        op = rng.choice([0, 1, 2, 2, 9, 10])
+        n = rng.choice(sizes)
+        if op >= 8:
+            n = min(n, 125)
+        key = bytes(rng.randrange(256) for _ in range(4))
+        h = orc.Hdr(fin=1 if op >= 8 else rng.randrange(2), rsv1=rng.randrange(2) if op < 8 else 0,
+                    opcode=op, mask=1, maskey=key, length=n)
+        payload = bytes(rng.randrange(256) for _ in range(n))
+        out += orc.encode_header(h) + orc.mask_bytes(key, payload)
+    return out
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 7, 1000, 4096, 65536])
+def test_masked_streams_match_oracle(chunk):
+    stream = masked_stream(chunk + 1, 8 if chunk == 1 else 80)
+    assert run_kmws(stream, kmws.SERVER, chunk, inplace=True) == \
+        run_oracle(stream, orc.SERVER, chunk, inplace=True)
+
+
+def test_close_then_trailing_and_error_sequences():
+    key = b"\x01\x02\x03\x04"
+    close = orc.encode_header(orc.Hdr(opcode=8, mask=1, maskey=key, length=2)) + orc.mask_bytes(key, b"\x03\xe8")
+    data = orc.encode_header(orc.Hdr(opcode=1, mask=1, maskey=key, length=5)) + orc.mask_bytes(key, b"Hello")
+    for stream in (data + close + data, data + b"\x09\x00" + data, data + b"\x81\x05Hello"):
+        for chunk in (0, 3):
+            assert run_kmws(stream, kmws.SERVER, chunk, True) == run_oracle(stream, orc.SERVER, chunk, True)
+
+
+def test_callback_destroy_stops_delivery():
+    stream = masked_stream(99, 10, sizes=(5, 100, 3000))
+    d = orc.Decoder(orc.SERVER)
+    d.destroy_on = 3
+    r_o = d.feed(stream)
+    h = kmws.WSHandler(kmws.SERVER)
+    got = []
+
+    def cb(hd, p):
+        got.append(frame_key(hd, p))
+        return len(got) - 1 == 3
+
+    h.setFrameCallback(cb)
+    assert h.handleData(stream) == r_o == kmws.WS_DESTROYED
+    assert got == [f.key() for f in d.frames]
