@@ -58,6 +58,14 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 with the same
+    # SONAME (libamdhip64.so.7) as /opt/rocm's.  Whichever loads first is used
+    # by both, and torch only works on its own copy, so load torch first; our
+    # library then binds to that runtime and shares its streams and memory.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     path = _build.LIB
     if not _build.up_to_date():
         try:
