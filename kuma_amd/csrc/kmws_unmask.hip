@@ -130,7 +130,7 @@ template <int V>
 __global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
-                                                              const WsHead* __restrict__ head)
+                                                              const WsHead* __restrict__ head, uint32_t tile_base)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -138,8 +138,9 @@ __global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restric
     __shared__ uint32_t s_key[Cfg::kCap];
 
     if (head->status != 0) return;  // prep found a bad descriptor: touch nothing
-    const uint64_t tile_lo = (uint64_t)blockIdx.x * Cfg::kTile;
-    const uint32_t f = map[blockIdx.x];
+    const uint32_t tile = tile_base + blockIdx.x;
+    const uint64_t tile_lo = (uint64_t)tile * Cfg::kTile;
+    const uint32_t f = map[tile];
     if (tile_lo + Cfg::kTile <= span)
         unmask_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, f, s_off, s_end, s_key);
     else
@@ -183,7 +184,11 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
                                                                 uint32_t n, unsigned long long* mismatches)
 {
     __shared__ uint32_t s_first;
-    const uint64_t blk_lo = (uint64_t)blockIdx.x * kCheckBytes;
+    const uint64_t nblk = (bytes + kCheckBytes - 1) / kCheckBytes;
+    unsigned long long bad = 0;
+    for (uint64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const uint64_t blk_lo = blk * kCheckBytes;
+    __syncthreads();
     if (threadIdx.x == 0) {
         // first frame with off + len > blk_lo (binary search over sorted descs)
         uint32_t lo = 0, hi = n;
@@ -195,7 +200,6 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
     }
     __syncthreads();
     uint32_t f = s_first;
-    unsigned long long bad = 0;
     const uint64_t p0 = blk_lo + 16u * threadIdx.x;
     for (int k = 0; k < 16; ++k) {
         const uint64_t p = p0 + k;
@@ -207,6 +211,7 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
             expect ^= (uint8_t)(key >> (8 * ((p - d[f].off) & 3)));
         }
         bad += base[p] != expect;
+    }
     }
     if (bad) atomicAdd(mismatches, bad);
 }
@@ -257,8 +262,13 @@ static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* d
     if (st != KMWS_OK) return st;
     if (n == 0 || span == 0) return KMWS_OK;
     const WsHead* head = static_cast<const WsHead*>(workspace);
-    hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3((uint32_t)ntiles), dim3(kBlock), 0, s, base, span, descs, n,
-                       reinterpret_cast<const uint32_t*>(head + 1), head);
+    // A launch may hold at most 2^32 work-items: split huge spans into pieces.
+    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
+    for (uint64_t t0 = 0; t0 < ntiles; t0 += kMaxBlocks) {
+        const uint64_t nb = ntiles - t0 < kMaxBlocks ? ntiles - t0 : kMaxBlocks;
+        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs, n,
+                           reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
+    }
     return hip_status(hipGetLastError());
 }
 
@@ -361,8 +371,8 @@ kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t se
 {
     if ((!base && bytes) || !mismatches) return KMWS_ERR_INVALID_PARAM;
     if (bytes == 0) return KMWS_OK;
-    const uint64_t nb = (bytes + kCheckBytes - 1) / kCheckBytes;
-    if (nb > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    uint64_t nb = (bytes + kCheckBytes - 1) / kCheckBytes;
+    if (nb > 65536) nb = 65536;  // grid-stride beyond this
     hipLaunchKernelGGL(check_unmasked_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                        base, bytes, seed, descs, n, mismatches);
     return hip_status(hipGetLastError());
