@@ -51,7 +51,9 @@ __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __res
 
 template <int V, bool FULL>
 __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
-                                            const kmws_desc* __restrict__ d, uint32_t n, uint32_t f,
+                                            const kmws_desc* __restrict__ d, uint32_t n,
+                                            const uint32_t* __restrict__ map, uint32_t tile,
+                                            const WsHead* __restrict__ head,
                                             uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
 {
     using Cfg = UnmaskCfg<V>;
@@ -59,14 +61,36 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
 
     // 1) Issue every payload load of this lane before any metadata work.
     //    Full tiles load unconditionally so the loads stay back to back.
+    //    Payload is touched once: non-temporal loads/stores (measured +6%
+    //    on MI355X for this in-place stream, tools/membw_probe.hip).
     u32x4 v[V];
     u32x4 m[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-        if (FULL || a < tile_hi) v[i] = *reinterpret_cast<const u32x4*>(base + a);
+        if (FULL || a < tile_hi) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + a));
         else v[i] = u32x4{0, 0, 0, 0};
         m[i] = u32x4{0, 0, 0, 0};
+    }
+    // Metadata comes after the payload loads.  No early exit sits between the
+    // loads and their uses, so the compiler cannot sink the loads below the
+    // scalar metadata waits.  A bad plan (status != 0) stores nothing.
+    __builtin_amdgcn_sched_barrier(0);
+    const bool ok = head->status == 0;
+    uint32_t f = map[tile];
+
+    // Fast path: one frame covers the whole tile (every tile of a 64 KiB-frame
+    // arena).  The test reads block-uniform scalars only, so the branch is
+    // uniform and needs no LDS or barrier.
+    const kmws_desc d0 = d[f < n ? f : 0];
+    if (FULL && f < n && d0.off <= tile_lo && d0.off + d0.len >= tile_hi) {
+        const uint32_t r = rot_key(d0.key, d0.off);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
+            if (ok) __builtin_nontemporal_store(v[i] ^ r, reinterpret_cast<u32x4*>(base + a));
+        }
+        return;
     }
 
     // 2) Stage the descriptors of frames overlapping the tile, kCap per round.
@@ -121,8 +145,8 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
     for (int i = 0; i < V; ++i) {
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
         const u32x4 mm = m[i];
-        if ((FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
-            *reinterpret_cast<u32x4*>(base + a) = v[i] ^ mm;
+        if (ok && (FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
+            __builtin_nontemporal_store(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a));
     }
 }
 
@@ -137,14 +161,12 @@ __global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restric
     __shared__ uint64_t s_end[Cfg::kCap];
     __shared__ uint32_t s_key[Cfg::kCap];
 
-    if (head->status != 0) return;  // prep found a bad descriptor: touch nothing
     const uint32_t tile = tile_base + blockIdx.x;
     const uint64_t tile_lo = (uint64_t)tile * Cfg::kTile;
-    const uint32_t f = map[tile];
     if (tile_lo + Cfg::kTile <= span)
-        unmask_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, f, s_off, s_end, s_key);
+        unmask_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head, s_off, s_end, s_key);
     else
-        unmask_tile<V, false>(base, tile_lo, span, d, n, f, s_off, s_end, s_key);
+        unmask_tile<V, false>(base, tile_lo, span, d, n, map, tile, head, s_off, s_end, s_key);
 }
 
 // ---- synthetic fill: byte i = byte (i & 7) of splitmix64(seed + (i >> 3)) ----
