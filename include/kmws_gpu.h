@@ -148,6 +148,55 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
  * 0 = OK, 1 = descriptor precondition violated, 2 = header error seen. */
 kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream);
 
+/* ---- batched header pack / unpack (device) ---- */
+
+/* Workspace bytes for kmws_encode_batch / kmws_gather_unmask with n frames
+ * and an output capacity of dst_cap bytes. */
+size_t kmws_copy_workspace_size(uint32_t n, uint64_t dst_cap);
+
+/* Batched frame encode: for frame i, WSHandler::encodeFrameHeader
+ * (WSHandler.cpp:46-106) of {flags[i], len, key} followed by the payload
+ * src[descs[i].off .. +len) masked with key when flags[i] & KMWS_FLAG_MASK
+ * (WebSocketImpl.cpp:381-404), all frames back to back in dst.  wire_off
+ * (n+1 entries, device) receives each frame's header offset and, in
+ * wire_off[n], the total wire size.  If the total exceeds dst_cap nothing is
+ * written and the workspace status word is set.  src and dst 16-B aligned;
+ * source payloads may overlap or sit anywhere in src. */
+kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const uint16_t* flags, uint32_t n,
+                              uint8_t* dst, uint64_t dst_cap, uint64_t* wire_off, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
+/* Workspace bytes for kmws_unpack_headers. */
+size_t kmws_unpack_workspace_size(void);
+
+/* Descriptor-indexed header unpack + validation, one frame per hdr_off entry
+ * (offsets ascending, each frame ending by the next header): the HDR1..MASKEY
+ * rules of WSHandler::decodeFrame (WSHandler.cpp:118-234) for `mode`,
+ * including the 127-class length quirk.  Per frame: out_desc = {payload
+ * offset in wire, len, key (0 if unmasked)}, out_flags = header byte 0 |
+ * mask << 8 (may be NULL), out_err = WSError (may be NULL): 1 truncated,
+ * 6 bad length, 7 protocol error, 5 frame overruns the next header.  Error
+ * frames get len 0.  Any error sets status bit 2. */
+kmws_status kmws_unpack_headers(const uint8_t* wire, uint64_t wire_len, const uint64_t* hdr_off, uint32_t n,
+                                int mode, kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Out-of-place unmask: frame i's payload src[descs[i].off .. +len) XOR its key
+ * is written densely to dst at dst_off[i] (exclusive scan of len; n+1
+ * entries, dst_off[n] = total).  Nothing is written if total > dst_cap. */
+kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint32_t n, uint8_t* dst,
+                               uint64_t dst_cap, uint64_t* dst_off, void* workspace, size_t workspace_bytes,
+                               void* stream);
+
+/* Host: walk the header chain of a wire image (WSHandler.cpp:108-280 state
+ * order, reading only header bytes and skipping payloads) and record each
+ * header offset.  Stops after `cap` frames, after a frame that is truncated
+ * or has an invalid length (recorded, so kmws_unpack_headers reports it), or
+ * after a CLOSE frame (the reference stops parsing there, :265-268).
+ * *consumed = bytes covered by the recorded complete frames. */
+kmws_status kmws_find_headers(const uint8_t* wire, uint64_t len, uint64_t* hdr_off, uint32_t cap,
+                              uint32_t* n_out, uint64_t* consumed);
+
 /* ---- synthetic data + checks (bench / test support, device side) ---- */
 
 /* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */

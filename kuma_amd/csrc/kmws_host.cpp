@@ -248,6 +248,44 @@ int kmws_encode_header(const kmws_frame_hdr* h, uint8_t out[KMWS_MAX_HEADER_SIZE
     return n;
 }
 
+// Header chain walk (boundary discovery) over complete frames.  Lengths use
+// the reference's semantics (127-class quirk, 10 MiB cap) so the chain is the
+// one WSHandler would follow.
+kmws_status kmws_find_headers(const uint8_t* wire, uint64_t len, uint64_t* hdr_off, uint32_t cap,
+                              uint32_t* n_out, uint64_t* consumed)
+{
+    if (!n_out || (len && !wire) || (cap && !hdr_off)) return KMWS_ERR_INVALID_PARAM;
+    uint64_t p = 0, done = 0;
+    uint32_t n = 0;
+    while (p < len && n < cap) {
+        hdr_off[n++] = p;
+        if (p + 2 > len) break;
+        const uint8_t b0 = wire[p], b1 = wire[p + 1];
+        const uint32_t plen = b1 & 0x7F, mask = b1 >> 7;
+        const uint64_t ext = plen == 126 ? 2 : (plen == 127 ? 8 : 0);
+        if (p + 2 + ext > len) break;
+        uint64_t L;
+        if (plen == 126) {
+            L = ((uint32_t)wire[p + 2] << 8) | wire[p + 3];
+        } else if (plen == 127) {
+            uint64_t x = 0;
+            for (uint32_t k = 0; k < 8; ++k)
+                x |= (uint64_t)(int64_t)(int32_t)((uint32_t)wire[p + 2 + k] << (((7u - k) * 8u) & 31u));
+            if ((x >> 63) != 0 || (uint32_t)x > KMWS_MAX_FRAME_DATA_LENGTH) break;
+            L = (uint32_t)x;
+        } else {
+            L = plen;
+        }
+        const uint64_t end = p + 2 + ext + (mask ? 4 : 0) + L;
+        if (end > len) break;
+        p = done = end;
+        if ((b0 & 0x0F) == KMWS_OP_CLOSE) break;
+    }
+    *n_out = n;
+    if (consumed) *consumed = done;
+    return KMWS_OK;
+}
+
 kmws_decoder* kmws_decoder_create(int mode, int device)
 {
     kmws_decoder* d = new (std::nothrow) kmws_decoder();

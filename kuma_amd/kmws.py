@@ -32,7 +32,8 @@ EXPORTS = [
     "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
     "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
     "kmws_unmask_batch_variant", "kmws_read_status", "kmws_fill_synthetic",
-    "kmws_fill_uniform_descs", "kmws_check_unmasked",
+    "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
+    "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
 ]
 
 
@@ -95,6 +96,12 @@ def lib() -> C.CDLL:
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
         "kmws_fill_uniform_descs": (i32, [vp, u32, u64, u32, u64, vp]),
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
+        "kmws_copy_workspace_size": (sz, [u32, u64]),
+        "kmws_encode_batch": (i32, [u8p, vp, vp, u32, u8p, u64, vp, vp, sz, vp]),
+        "kmws_unpack_workspace_size": (sz, []),
+        "kmws_unpack_headers": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, vp]),
+        "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
+        "kmws_find_headers": (i32, [u8p, u64, vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -294,3 +301,44 @@ def check_unmasked(base, seed: int, descs, nbytes: Optional[int] = None, stream=
     _check(lib().kmws_check_unmasked(base.data_ptr(), nbytes, seed, descs.data_ptr(), descs.shape[0],
                                      cnt.data_ptr(), _stream_handle(stream)), "kmws_check_unmasked")
     return int(cnt.item())
+
+
+# ---- pack / unpack ----
+
+def copy_workspace_size(n: int, dst_cap: int) -> int:
+    return lib().kmws_copy_workspace_size(n, dst_cap)
+
+
+def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None) -> None:
+    """kmws_encode_batch: descs (n,2) int64, flags int16 (n,), wire_off int64 (n+1,)."""
+    _check(lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), flags.data_ptr(), descs.shape[0],
+                                   dst.data_ptr(), dst.numel(), wire_off.data_ptr(), ws.ptr, ws.nbytes,
+                                   _stream_handle(stream)), "kmws_encode_batch")
+
+
+def unpack_headers(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: Workspace,
+                   wire_len: Optional[int] = None, stream=None) -> None:
+    wire_len = wire.numel() if wire_len is None else wire_len
+    _check(lib().kmws_unpack_headers(wire.data_ptr(), wire_len, hdr_off.data_ptr(), hdr_off.shape[0], mode,
+                                     out_desc.data_ptr(),
+                                     out_flags.data_ptr() if out_flags is not None else None,
+                                     out_err.data_ptr() if out_err is not None else None,
+                                     ws.ptr, ws.nbytes, _stream_handle(stream)), "kmws_unpack_headers")
+
+
+def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
+    _check(lib().kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), descs.shape[0], dst.data_ptr(),
+                                    dst.numel(), dst_off.data_ptr(), ws.ptr, ws.nbytes,
+                                    _stream_handle(stream)), "kmws_gather_unmask")
+
+
+def find_headers(wire: bytes, cap: Optional[int] = None):
+    """Host header-chain walk -> (list of header offsets, consumed bytes)."""
+    import numpy as np
+    buf = np.frombuffer(bytes(wire), dtype=np.uint8) if len(wire) else np.zeros(1, np.uint8)
+    cap = len(wire) // 2 + 1 if cap is None else cap
+    out = np.zeros(max(1, cap), dtype=np.uint64)
+    n, used = C.c_uint32(0), C.c_uint64(0)
+    _check(lib().kmws_find_headers(buf.ctypes.data, len(wire), out.ctypes.data, cap, C.byref(n),
+                                   C.byref(used)), "kmws_find_headers")
+    return out[:n.value].tolist(), used.value

@@ -112,3 +112,26 @@ def test_synthetic_host_generator():
     assert (a[13:53] == b).all()
     w = orc.splitmix64(5 + 1).to_bytes(8, "little")
     assert bytes(a[8:16]) == w
+
+
+def test_find_headers_matches_oracle_walk():
+    rng = random.Random(21)
+    stream, offs = b"", []
+    for _ in range(200):
+        n = rng.choice([0, 1, 125, 126, 65535, 65536, 70000])
+        h = orc.encode_header(orc.Hdr(opcode=rng.choice([0, 1, 2]), mask=rng.randrange(2),
+                                      maskey=b"abcd", length=n))
+        offs.append(len(stream))
+        stream += h + bytes(n)
+    got, used = kmws.find_headers(stream)
+    assert got == offs and used == len(stream)
+    # truncated tail: last frame recorded, consumed stops before it
+    got, used = kmws.find_headers(stream[:-1])
+    assert got == offs and used == offs[-1]
+    # CLOSE stops the walk (WSHandler.cpp:265-268)
+    close = orc.encode_header(orc.Hdr(opcode=8, length=0))
+    got, used = kmws.find_headers(close + stream)
+    assert got == [0] and used == 2
+    # invalid 127-class length is recorded and ends the walk
+    got, _ = kmws.find_headers(bytes.fromhex("827f4000000000000000") + stream)
+    assert got == [0]
