@@ -197,6 +197,22 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
 kmws_status kmws_find_headers(const uint8_t* wire, uint64_t len, uint64_t* hdr_off, uint32_t cap,
                               uint32_t* n_out, uint64_t* consumed);
 
+/* ---- host-resident batches: pinned H2D -> kernel -> D2H pipeline ---- */
+typedef struct kmws_pipeline kmws_pipeline;
+
+/* depth slots (streams) of chunk_bytes device buffer each; chunks are cut on
+ * frame boundaries with at most max_frames_per_chunk frames. */
+kmws_pipeline* kmws_pipeline_create(int device, uint64_t chunk_bytes, uint32_t max_frames_per_chunk, int depth);
+void           kmws_pipeline_destroy(kmws_pipeline* p);
+
+/* In-place unmask of frames that live in HOST memory (descs on the host,
+ * offsets relative to host_base, sorted, within span).  Synchronous: returns
+ * when every byte is back in host_base.  Pin host_base (hipHostMalloc /
+ * hipHostRegister) for full PCIe rate.  Only the frames' extents are written
+ * back. */
+kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t span, const kmws_desc* descs,
+                                 uint32_t n);
+
 /* ---- synthetic data + checks (bench / test support, device side) ---- */
 
 /* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */

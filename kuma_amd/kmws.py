@@ -34,6 +34,7 @@ EXPORTS = [
     "kmws_unmask_batch_variant", "kmws_read_status", "kmws_fill_synthetic",
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
+    "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask",
 ]
 
 
@@ -101,6 +102,9 @@ def lib() -> C.CDLL:
         "kmws_unpack_workspace_size": (sz, []),
         "kmws_unpack_headers": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, vp]),
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
+        "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
+        "kmws_pipeline_destroy": (None, [vp]),
+        "kmws_pipeline_unmask": (i32, [vp, u8p, u64, vp, u32]),
         "kmws_find_headers": (i32, [u8p, u64, vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
@@ -342,3 +346,28 @@ def find_headers(wire: bytes, cap: Optional[int] = None):
     _check(lib().kmws_find_headers(buf.ctypes.data, len(wire), out.ctypes.data, cap, C.byref(n),
                                    C.byref(used)), "kmws_find_headers")
     return out[:n.value].tolist(), used.value
+
+
+class Pipeline:
+    """kmws_pipeline: host-resident in-place unmask through pinned H2D/D2H."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 64 << 20, max_frames: int = 1 << 16,
+                 depth: int = 3):
+        self._p = lib().kmws_pipeline_create(device, chunk_bytes, max_frames, depth)
+        if not self._p:
+            raise RuntimeError("kmws_pipeline_create failed (no gfx950 device or bad arguments)")
+
+    def unmask(self, host_u8, descs_np) -> None:
+        """host_u8: numpy uint8 array or pinned torch CPU tensor; descs_np: DESC-layout numpy array."""
+        ptr = host_u8.data_ptr() if hasattr(host_u8, "data_ptr") else host_u8.ctypes.data
+        span = host_u8.numel() if hasattr(host_u8, "numel") else host_u8.nbytes
+        _check(lib().kmws_pipeline_unmask(self._p, ptr, span, descs_np.ctypes.data, len(descs_np)),
+               "kmws_pipeline_unmask")
+
+    def __del__(self):
+        try:
+            if getattr(self, "_p", None):
+                lib().kmws_pipeline_destroy(self._p)
+                self._p = None
+        except Exception:
+            pass

@@ -1,0 +1,60 @@
+"""Host-resident batches through kmws_pipeline (pinned H2D -> unmask -> D2H),
+bit-exact vs the oracle; small chunks force many frame-boundary cuts."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def kmws():
+    from kuma_amd import kmws as k
+    if k.device_count() < 1:
+        pytest.fail("gpu test needs a gfx950 device")
+    return k
+
+
+def wire_like(rng, n, maxlen):
+    lens = rng.integers(0, maxlen, size=n)
+    hdr = rng.integers(2, 15, size=n)
+    starts = np.cumsum(np.concatenate([[0], hdr + lens]))
+    offs = (starts[:-1] + hdr).astype(np.uint64)
+    buf = rng.integers(0, 256, size=int(starts[-1]) + 7, dtype=np.uint8)
+    d = np.zeros(n, dtype=orc.DESC_DTYPE)
+    d["off"], d["len"] = offs, lens
+    d["key"] = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    return buf, d
+
+
+@pytest.mark.parametrize("chunk,max_frames,depth", [(65536, 1 << 16, 2), (70000, 7, 3), (1 << 20, 100, 1)])
+def test_pipeline_pageable(kmws, chunk, max_frames, depth):
+    rng = np.random.default_rng(chunk + max_frames)
+    buf, d = wire_like(rng, 700, 60000)
+    want = buf.copy()
+    orc.unmask_batch(want, d)
+    p = kmws.Pipeline(0, chunk, max_frames, depth)
+    p.unmask(buf, d)
+    assert np.array_equal(buf, want)
+
+
+def test_pipeline_pinned(kmws):
+    import torch
+    rng = np.random.default_rng(9)
+    buf, d = wire_like(rng, 3000, 70000)
+    want = buf.copy()
+    orc.unmask_batch(want, d)
+    t = torch.from_numpy(buf).pin_memory()
+    kmws.Pipeline(0, 8 << 20, 4096, 3).unmask(t, d)
+    assert np.array_equal(t.numpy(), want)
+
+
+def test_pipeline_rejects_oversized_frame(kmws):
+    rng = np.random.default_rng(1)
+    buf, d = wire_like(rng, 3, 100)
+    d["len"][1] = 200000
+    buf = np.zeros(int(d["off"][-1]) + 300000, np.uint8)
+    d["off"][2] = d["off"][1] + 200010
+    with pytest.raises(RuntimeError):
+        kmws.Pipeline(0, 65536, 16, 2).unmask(buf, d)
