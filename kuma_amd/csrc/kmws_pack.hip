@@ -203,42 +203,54 @@ struct CopyLds {
     uint32_t hl[kCopyCap];
 };
 
-__device__ __forceinline__ uint32_t pick(const u32x4& lo, const u32x4& hi, int k)
+// Dword I of the 8-dword window lo||hi (I fixed at compile time).
+template <int I>
+__device__ __forceinline__ uint32_t dw(const u32x4& lo, const u32x4& hi)
 {
-    switch (k) {
-    case 0: return lo.x;
-    case 1: return lo.y;
-    case 2: return lo.z;
-    case 3: return lo.w;
-    case 4: return hi.x;
-    case 5: return hi.y;
-    case 6: return hi.z;
-    default: return hi.w;
-    }
+    if constexpr (I == 0) return lo.x;
+    else if constexpr (I == 1) return lo.y;
+    else if constexpr (I == 2) return lo.z;
+    else if constexpr (I == 3) return lo.w;
+    else if constexpr (I == 4) return hi.x;
+    else if constexpr (I == 5) return hi.y;
+    else if constexpr (I == 6) return hi.z;
+    else return hi.w;
+}
+
+// Dword q + K of the window for q in 0..3 (per lane): a select chain over
+// distinct registers (an indexed register array would be placed in scratch).
+template <int K>
+__device__ __forceinline__ uint32_t pick(const u32x4& lo, const u32x4& hi, uint32_t q)
+{
+    const uint32_t a = (q & 1u) ? dw<K + 1>(lo, hi) : dw<K>(lo, hi);
+    const uint32_t b = (q & 1u) ? dw<K + 3>(lo, hi) : dw<K + 2>(lo, hi);
+    return (q & 2u) ? b : a;
 }
 
 // 16 bytes starting at byte delta (0..15) of the 32-byte window lo||hi.
 __device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t delta)
 {
-    const int q = (int)(delta >> 2);
+    const uint32_t q = delta >> 2;
     const uint32_t r = (delta & 3u) * 8u;
-    u32x4 o;
-    uint32_t c0 = pick(lo, hi, q), c1 = pick(lo, hi, q + 1), c2 = pick(lo, hi, q + 2), c3 = pick(lo, hi, q + 3),
-             c4 = pick(lo, hi, q + 4);
-    if (r == 0) {
-        o = u32x4{c0, c1, c2, c3};
-    } else {
-        o.x = __builtin_amdgcn_alignbit(c1, c0, r);
-        o.y = __builtin_amdgcn_alignbit(c2, c1, r);
-        o.z = __builtin_amdgcn_alignbit(c3, c2, r);
-        o.w = __builtin_amdgcn_alignbit(c4, c3, r);
-    }
-    return o;
+    const uint32_t c0 = pick<0>(lo, hi, q), c1 = pick<1>(lo, hi, q), c2 = pick<2>(lo, hi, q),
+                   c3 = pick<3>(lo, hi, q), c4 = pick<4>(lo, hi, q);
+    // v_alignbit_b32(hi, lo, 0) == lo, so r == 0 needs no special case
+    return u32x4{__builtin_amdgcn_alignbit(c1, c0, r), __builtin_amdgcn_alignbit(c2, c1, r),
+                 __builtin_amdgcn_alignbit(c3, c2, r), __builtin_amdgcn_alignbit(c4, c3, r)};
 }
 
-__device__ __forceinline__ uint8_t hdr_byte(uint64_t h0, uint64_t h1, uint32_t k)
+// W[k] = h[k - s] (0 where k - s is outside 0..15), s in [-15, 15].
+__device__ __forceinline__ u32x4 shift_in(const u32x4& h, int s)
 {
-    return (uint8_t)((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8))) & 0xFFu);
+    const u32x4 z = u32x4{0, 0, 0, 0};
+    if (s == 0) return h;
+    return s > 0 ? funnel16(z, h, (uint32_t)(16 - s)) : funnel16(h, z, (uint32_t)(-s));
+}
+
+__device__ __forceinline__ u32x4 byte_range(int lo, int hi)
+{
+    return u32x4{dword_byte_mask(lo, hi, 0), dword_byte_mask(lo, hi, 1), dword_byte_mask(lo, hi, 2),
+                 dword_byte_mask(lo, hi, 3)};
 }
 
 // Fill a CopyLds row for frame fi; returns the region end.
@@ -354,33 +366,25 @@ __global__ void __launch_bounds__(kBlock) mask_copy_kernel(const uint8_t* __rest
                 if (r0 >= a + 16) break;
                 const uint32_t hlj = L.hl[j], lenj = L.len[j];
                 const uint64_t p0 = r0 + hlj, r1 = p0 + lenj;
-                const uint32_t kj = L.key[j];
-                const uint64_t sj = L.src[j];
-                if (p0 <= a && r1 >= a + 16) {  // whole word is payload of frame j
-                    const uint64_t sb = sj + (a - p0);
-                    const uint32_t delta = (uint32_t)(sb & 15u);
-                    const u32x4 l0 = *reinterpret_cast<const u32x4*>(src + (sb - delta));
-                    const u32x4 h0 = delta ? *reinterpret_cast<const u32x4*>(src + (sb - delta) + 16) : l0;
-                    out[i] = (delta ? funnel16(l0, h0, delta) : l0) ^ rot_key(kj, p0);
-                    continue;
+                // header bytes [r0, p0) of frame j that fall in this word
+                if (HEADERS && p0 > a) {
+                    const int s = (int)((int64_t)r0 - (int64_t)a);
+                    const uint64_t h0 = L.h0[j], h1 = L.h1[j];
+                    const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+                    out[i] |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, s + (int)hlj > 16 ? 16 : s + (int)hlj);
                 }
-                const uint64_t e = r1 < a + 16 ? r1 : a + 16;
-                for (uint64_t p = r0 > a ? r0 : a; p < e; ++p) {
-                    uint32_t b;
-                    if (p < p0) {
-                        b = hdr_byte(L.h0[j], L.h1[j], (uint32_t)(p - r0));
-                    } else {
-                        const uint64_t q = p - p0;
-                        b = src[sj + q] ^ ((kj >> (8 * (q & 3))) & 0xFFu);
-                    }
-                    const uint32_t k = (uint32_t)(p - a);
-                    const uint32_t sh = 8u * (k & 3u);
-                    switch (k >> 2) {
-                    case 0: out[i].x |= b << sh; break;
-                    case 1: out[i].y |= b << sh; break;
-                    case 2: out[i].z |= b << sh; break;
-                    default: out[i].w |= b << sh; break;
-                    }
+                // payload bytes [max(a, p0), min(a + 16, r1)) of frame j
+                if (lenj && p0 < a + 16 && r1 > a) {
+                    const uint64_t lo_b = p0 > a ? p0 : a, hi_b = r1 < a + 16 ? r1 : a + 16;
+                    const uint64_t sj = L.src[j];
+                    const uint64_t slo = sj + (lo_b - p0), shi = sj + (hi_b - p0);
+                    const uint64_t w0 = slo & ~(uint64_t)15, w1 = (shi - 1) & ~(uint64_t)15;
+                    const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + w0);
+                    const u32x4 W1 = w1 != w0 ? *reinterpret_cast<const u32x4*>(src + w1) : W0;
+                    const int d = (int)((int64_t)(sj + a - p0) - (int64_t)w0);  // in [-15, 15]
+                    const u32x4 V = d >= 0 ? funnel16(W0, W1, (uint32_t)d)
+                                           : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + d));
+                    out[i] |= (V ^ rot_key(L.key[j], p0)) & byte_range((int)(lo_b - a), (int)(hi_b - a));
                 }
             }
         }
@@ -394,8 +398,12 @@ __global__ void __launch_bounds__(kBlock) mask_copy_kernel(const uint8_t* __rest
         if (a + 16 <= tile_hi) {
             __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + a));
         } else if (a < tile_hi) {  // last partial word of the output: byte stores
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(&out[i]);
-            for (uint64_t p = a; p < tile_hi; ++p) dst[p] = (uint8_t)(w[(p - a) >> 2] >> (8 * ((p - a) & 3)));
+            const u32x4 o = out[i];
+            for (uint64_t p = a; p < tile_hi; ++p) {
+                const uint32_t k = (uint32_t)(p - a);
+                const uint32_t dw = (k & 8u) ? ((k & 4u) ? o.w : o.z) : ((k & 4u) ? o.y : o.x);
+                dst[p] = (uint8_t)(dw >> (8 * (k & 3u)));
+            }
         }
     }
 }
