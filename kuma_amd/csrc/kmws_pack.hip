@@ -354,34 +354,6 @@ __global__ void __launch_bounds__(kBlock) mask_copy_kernel(const uint8_t* __rest
 #pragma unroll
         for (int i = 0; i < kCopyV; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-            // Wave fast path: this wave's 1 KiB of output lies inside one payload
-            // (wave-uniform test), so one aligned load per lane + a neighbour
-            // shuffle feed the funnel shift, as in the tile fast path.
-            {
-                const uint64_t wa = tile_lo + 16u * (uint64_t)((tid & ~63) + kBlock * i);
-                int lo = 0, hi = cnt;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (L.dst[mid] + L.hl[mid] + L.len[mid] <= wa) lo = mid + 1; else hi = mid;
-                }
-                const int jw = lo;
-                const uint64_t p0w = jw < cnt ? L.dst[jw] + L.hl[jw] : ~0ull;
-                if (jw < cnt && p0w <= wa && p0w + L.len[jw] >= wa + 1024 && wa + 1024 <= tile_hi) {
-                    const uint64_t sbase = L.src[jw] + (wa - p0w);
-                    const uint32_t delta = (uint32_t)(sbase & 15u);
-                    const uint8_t* s0 = src + (sbase - delta);
-                    const int lane = tid & 63;
-                    const u32x4 lw = *reinterpret_cast<const u32x4*>(s0 + 16 * lane);
-                    u32x4 nx;
-                    nx.x = __shfl_down(lw.x, 1, 64);
-                    nx.y = __shfl_down(lw.y, 1, 64);
-                    nx.z = __shfl_down(lw.z, 1, 64);
-                    nx.w = __shfl_down(lw.w, 1, 64);
-                    if (lane == 63) nx = delta ? *reinterpret_cast<const u32x4*>(s0 + 16 * 64) : lw;
-                    out[i] = funnel16(lw, nx, delta) ^ rot_key(L.key[jw], p0w);
-                    continue;
-                }
-            }
             if (a >= tile_hi) continue;
             // first staged frame whose region ends after a
             int lo = 0, hi = cnt;
