@@ -49,9 +49,9 @@ def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
     workload: 4096 x frame_len frames, repeated for ~`seconds`."""
     import numpy as np
     from oracle import oracle as orc
-    n = 4096
+    n = 16384  # 1 GiB of 64 KiB frames: 4x the host's L3, so the sample streams from DRAM
     rng = np.random.default_rng(seed)
-    base = rng.integers(0, 256, size=n * frame_len, dtype=np.uint8)
+    base = np.frombuffer(rng.bytes(n * frame_len), dtype=np.uint8).copy()
     descs = np.zeros(n, dtype=orc.DESC_DTYPE)
     descs["off"] = np.arange(n, dtype=np.uint64) * frame_len
     descs["len"] = frame_len
@@ -115,10 +115,16 @@ def main():
     if kmws.device_count() < 1:
         raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
 
+    from kuma_amd import shard
     n, L = a.frames, a.frame_len
     span = n * L
-    seed = a.seed + rank * 0x1000003  # each rank owns a distinct shard
-    key_seed = seed ^ 0x5EED
+    # Weak scaling: the job is world x n frames; rank g owns global frames
+    # [g*n, (g+1)*n) (kuma_amd/shard.py).  Data and keys are generated from
+    # global positions, so the shards are slices of one big batch.
+    g_lo, g_hi = shard.uniform_range(n * world, rank, world)
+    assert g_hi - g_lo == n
+    seed = a.seed + (g_lo * L >> 3)
+    key_seed = (a.seed ^ 0x5EED) + g_lo
     base = torch.empty(span, dtype=torch.uint8, device=dev)
     descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span), device=dev)
@@ -178,7 +184,7 @@ def main():
 
     ms_per_step = elapsed * 1e3 / a.steps
     total_payload = world * span
-    value = total_payload / (elapsed / a.steps) / 2**30
+    value = shard.aggregate_rate([span * a.steps] * world, [elapsed] * world) / 2**30
     alg_bytes = n * (2 * L + DESC_BYTES)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = traffic_from_profile(n, L)
