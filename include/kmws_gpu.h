@@ -205,11 +205,17 @@ typedef struct kmws_pipeline kmws_pipeline;
 kmws_pipeline* kmws_pipeline_create(int device, uint64_t chunk_bytes, uint32_t max_frames_per_chunk, int depth);
 void           kmws_pipeline_destroy(kmws_pipeline* p);
 
+/* Transfer mode: AUTO = zero-copy when host_base is pinned (hipHostMalloc /
+ * hipHostRegister; the kernel reads and writes host memory over PCIe), else
+ * chunked SDMA copies through device slots; COPY forces the chunked SDMA
+ * path; ZEROCOPY requires pinned memory. */
+enum kmws_xfer { KMWS_XFER_AUTO = 0, KMWS_XFER_COPY = 1, KMWS_XFER_ZEROCOPY = 2 };
+kmws_status kmws_pipeline_set_transfer(kmws_pipeline* p, int mode);
+
 /* In-place unmask of frames that live in HOST memory (descs on the host,
  * offsets relative to host_base, sorted, within span).  Synchronous: returns
- * when every byte is back in host_base.  Pin host_base (hipHostMalloc /
- * hipHostRegister) for full PCIe rate.  Only the frames' extents are written
- * back. */
+ * when every byte is back in host_base.  Only the frames' extents are written
+ * back by the copy path; the zero-copy path rewrites their 16-B hulls. */
 kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t span, const kmws_desc* descs,
                                  uint32_t n);
 

@@ -34,7 +34,7 @@ EXPORTS = [
     "kmws_unmask_batch_variant", "kmws_read_status", "kmws_fill_synthetic",
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
-    "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask",
+    "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
 ]
 
 
@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
         "kmws_pipeline_destroy": (None, [vp]),
+        "kmws_pipeline_set_transfer": (i32, [vp, i32]),
         "kmws_pipeline_unmask": (i32, [vp, u8p, u64, vp, u32]),
         "kmws_find_headers": (i32, [u8p, u64, vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     }
@@ -351,11 +352,14 @@ def find_headers(wire: bytes, cap: Optional[int] = None):
 class Pipeline:
     """kmws_pipeline: host-resident in-place unmask through pinned H2D/D2H."""
 
+    AUTO, COPY, ZEROCOPY = 0, 1, 2
+
     def __init__(self, device: int = 0, chunk_bytes: int = 64 << 20, max_frames: int = 1 << 16,
-                 depth: int = 3):
+                 depth: int = 3, transfer: int = 0):
         self._p = lib().kmws_pipeline_create(device, chunk_bytes, max_frames, depth)
         if not self._p:
             raise RuntimeError("kmws_pipeline_create failed (no gfx950 device or bad arguments)")
+        _check(lib().kmws_pipeline_set_transfer(self._p, transfer), "kmws_pipeline_set_transfer")
 
     def unmask(self, host_u8, descs_np) -> None:
         """host_u8: numpy uint8 array or pinned torch CPU tensor; descs_np: DESC-layout numpy array."""

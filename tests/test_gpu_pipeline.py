@@ -39,15 +39,24 @@ def test_pipeline_pageable(kmws, chunk, max_frames, depth):
     assert np.array_equal(buf, want)
 
 
-def test_pipeline_pinned(kmws):
+@pytest.mark.parametrize("transfer", [0, 1, 2])
+def test_pipeline_pinned(kmws, transfer):
+    """AUTO/ZEROCOPY: the kernel works on pinned host memory over PCIe; COPY: SDMA ring."""
     import torch
-    rng = np.random.default_rng(9)
+    rng = np.random.default_rng(9 + transfer)
     buf, d = wire_like(rng, 3000, 70000)
     want = buf.copy()
     orc.unmask_batch(want, d)
     t = torch.from_numpy(buf).pin_memory()
-    kmws.Pipeline(0, 8 << 20, 4096, 3).unmask(t, d)
+    kmws.Pipeline(0, 8 << 20, 4096, 3, transfer=transfer).unmask(t, d)
     assert np.array_equal(t.numpy(), want)
+
+
+def test_pipeline_zerocopy_needs_pinned(kmws):
+    rng = np.random.default_rng(2)
+    buf, d = wire_like(rng, 10, 1000)
+    with pytest.raises(RuntimeError):
+        kmws.Pipeline(0, 1 << 20, 64, 2, transfer=2).unmask(buf, d)
 
 
 def test_pipeline_rejects_oversized_frame(kmws):
