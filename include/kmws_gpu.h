@@ -107,9 +107,34 @@ void          kmws_decoder_reset(kmws_decoder* dec);                /* WSHandler
 /* WSHandler::handleData (WSHandler.cpp:41-44 -> decodeFrame :108-280).
  * Same return values and callback sequence; masked payloads are unmasked by
  * the GPU (one batched launch per call) and, as in kuma, in place in `data`
- * when a frame lies wholly inside it.  Returns a kmws_ws_error value, or a
- * negative kmws_status if the GPU step failed. */
+ * when a frame lies wholly inside it.  If `data` is pinned host memory the
+ * kernel unmasks it there directly (zero-copy, rewriting the 16-B hulls of
+ * those payloads); otherwise payloads go through a pinned staging copy.
+ * Returns a kmws_ws_error value, or a negative kmws_status if the GPU step
+ * failed. */
 int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_cb cb, void* user);
+
+/* ---- deferred delivery: one GPU batch per event-loop iteration (SURVEY f-1) ----
+ * kuma calls handleData once per 64 KiB socket read per connection; a GPU
+ * round trip per call costs more than the scalar unmask it replaces.  A loop
+ * thread instead feeds every read of every connection with
+ * kmws_decoder_feed_deferred (headers parsed and validated immediately, same
+ * return values as kmws_decoder_feed; payloads copied into the batch) and
+ * calls kmws_rx_batch_flush once per iteration: one GPU unmask over all
+ * staged payloads, then every deferred callback in feed order (the
+ * EventLoop::post pattern, kmapi.h:204-210).  Payload views point into the
+ * batch and are valid during the callback; the caller's chunk is not
+ * modified.  A callback returning nonzero ("destroyed") drops that decoder's
+ * remaining frames of the flush.  Destroy a decoder only after a flush or
+ * after kmws_rx_batch_discard. */
+typedef struct kmws_rx_batch kmws_rx_batch;
+kmws_rx_batch* kmws_rx_batch_create(int device);      /* NULL without a gfx950 device */
+void           kmws_rx_batch_destroy(kmws_rx_batch* b);
+int            kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_t* data, size_t len,
+                                          kmws_frame_cb cb, void* user);
+int            kmws_rx_batch_flush(kmws_rx_batch* b);  /* frames delivered, or negative status */
+int            kmws_rx_batch_pending(const kmws_rx_batch* b);
+void           kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec);
 
 /* ======================= device batch entries ======================= */
 

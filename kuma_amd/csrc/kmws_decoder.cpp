@@ -1,0 +1,438 @@
+// WSHandler-compatible streaming decoder of the kmws C ABI
+// (src/ws/WSHandler.{h,cpp} in the reference).
+//
+// The per-byte header state machine stays on the event-loop thread, as in kuma
+// (headers arrive byte-serially per connection, WSHandler.cpp:108-280).  The
+// payload work -- the reference's scalar unmask loop (WSHandler.cpp:303-310) --
+// runs on the GPU, batched:
+//   kmws_decoder_feed           one GPU batch per call, callbacks before return
+//                               (the drop-in for WSHandler::handleData);
+//   kmws_decoder_feed_deferred  frames of many calls / connections staged into
+//   + kmws_rx_batch_flush       a kmws_rx_batch; one GPU batch per flush (once
+//                               per event-loop iteration), callbacks at flush.
+// There is no CPU unmask path: without a usable gfx950 device a masked frame
+// fails the call with KMWS_ERR_NOT_SUPPORTED.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "kmws_gpu.h"
+#include "kmws_host_util.hpp"
+
+using namespace kmws;
+
+namespace {
+
+enum class St : uint8_t { HDR1, HDR2, HDREX, MASKEY, DATA, CLOSED, IN_ERROR };  // WSHandler.h:57-65
+
+bool is_control(uint8_t op) { return op >= 8; }  // WSHandler.h:52-54
+
+constexpr int kParsing = -100;
+
+// Where a completed frame's payload lives until delivery (synchronous feed).
+enum Origin : int {
+    kInChunk = 0,        // unmasked (or empty): view into the caller's chunk
+    kInChunkPinned = 1,  // masked, caller's chunk is pinned: unmasked there in place by the kernel
+    kInChunkStaged = 2,  // masked, pageable chunk: staged, written back in place before delivery
+    kStagedMasked = 3,   // masked, reassembled across chunks: view into staging
+    kHeld = 4,           // unmasked, reassembled: view into a held reassembly buffer
+};
+
+struct Pending {
+    kmws_frame_hdr hdr;
+    uint8_t* data_ptr;  // in-chunk kinds: payload position in the chunk
+    size_t stage_off;   // staged kinds: payload offset in the staging area
+    size_t hold_idx;    // kHeld: index into the held buffers
+    Origin where;
+};
+
+}  // namespace
+
+struct kmws_decoder {
+    int mode = KMWS_MODE_CLIENT;
+    int device = 0;
+    // DecodeContext (WSHandler.h:66-78)
+    kmws_frame_hdr hdr{};
+    St state = St::HDR1;
+    std::vector<uint8_t> buf;
+    uint8_t pos = 0;
+    // synchronous-feed delivery lists and staging
+    std::vector<Pending> pending;
+    std::vector<std::vector<uint8_t>> held;
+    std::vector<kmws_desc> chunk_descs;
+    PinnedStage stage;
+
+    void reset_ctx()  // DecodeContext::reset, WSHandler.h:66-72 (capacity kept)
+    {
+        std::memset(&hdr, 0, sizeof(hdr));
+        state = St::HDR1;
+        buf.clear();
+        pos = 0;
+    }
+};
+
+struct kmws_rx_batch {
+    struct Item {
+        kmws_decoder* dec;  // identity only; never dereferenced at flush
+        kmws_frame_cb cb;
+        void* user;
+        kmws_frame_hdr hdr;
+        size_t off;
+    };
+    PinnedStage stage;
+    std::vector<Item> items;
+    int device = 0;
+    bool flushing = false;  // feeding the batch from inside its own flush is refused
+};
+
+namespace {
+
+// The reference's decodeFrame loop (WSHandler.cpp:108-280).  At every
+// completed frame, sink(hdr, payload, reassembly) is called with the payload
+// contiguous in memory: in the caller's chunk (reassembly == nullptr) or in
+// the decoder's reassembly buffer (the sink may steal it).  Returns the
+// WSError of the call, or a negative status the sink returned.
+template <class Sink>
+int parse_chunk(kmws_decoder* dec, uint8_t* data, size_t len, Sink&& sink)
+{
+    int result = kParsing;
+    size_t p = 0;
+    auto& h = dec->hdr;
+    while (result == kParsing && p < len) {
+        switch (dec->state) {
+        case St::HDR1: {  // :118-135
+            const uint8_t b = data[p++];
+            h.fin = b >> 7;
+            h.opcode = b & 0x0F;
+            h.rsv1 = (b >> 6) & 1;
+            h.rsv2 = (b >> 5) & 1;
+            h.rsv3 = (b >> 4) & 1;
+            if (!h.fin && is_control(h.opcode)) {
+                dec->state = St::IN_ERROR;
+                result = KMWS_WS_PROTOCOL_ERROR;
+                break;
+            }
+            dec->state = St::HDR2;
+        }
+            [[fallthrough]];
+        case St::HDR2: {  // :136-156
+            if (p >= len) {
+                result = KMWS_WS_NEED_MORE_DATA;
+                break;
+            }
+            const uint8_t b = data[p++];
+            h.mask = b >> 7;
+            h.plen = b & 0x7F;
+            h.xpl64 = 0;
+            dec->pos = 0;
+            dec->buf.clear();
+            if (is_control(h.opcode) && h.plen > 125) {
+                dec->state = St::IN_ERROR;
+                result = KMWS_WS_PROTOCOL_ERROR;
+                break;
+            }
+            dec->state = St::HDREX;
+        }
+            [[fallthrough]];
+        case St::HDREX: {  // :157-204
+            if (h.plen == 126) {
+                for (; p < len && dec->pos < 2; ++p, ++dec->pos)
+                    h.xpl64 = (h.xpl64 & ~0xFFFFull) |
+                              (uint16_t)((uint16_t)h.xpl64 | (uint16_t)(data[p] << ((1 - dec->pos) * 8)));
+                if (dec->pos < 2) {
+                    result = KMWS_WS_NEED_MORE_DATA;
+                    break;
+                }
+                dec->pos = 0;
+                if ((uint16_t)h.xpl64 < 126) {
+                    dec->state = St::IN_ERROR;
+                    result = KMWS_WS_INVALID_LENGTH;
+                    break;
+                }
+                h.length = (uint16_t)h.xpl64;
+            } else if (h.plen == 127) {
+                // Reference quirk (WSHandler.cpp:179): a promoted 32-bit int
+                // shifted by (7-k)*8; x86-64 takes the count mod 32 and the
+                // int result is sign-extended into the u64.
+                for (; p < len && dec->pos < 8; ++p, ++dec->pos) {
+                    const uint32_t sh = ((7u - dec->pos) * 8u) & 31u;
+                    h.xpl64 |= (uint64_t)(int64_t)(int32_t)((uint32_t)data[p] << sh);
+                }
+                if (dec->pos < 8) {
+                    result = KMWS_WS_NEED_MORE_DATA;
+                    break;
+                }
+                dec->pos = 0;
+                if ((h.xpl64 >> 63) != 0) {
+                    dec->state = St::IN_ERROR;
+                    result = KMWS_WS_INVALID_LENGTH;
+                    break;
+                }
+                h.length = (uint32_t)h.xpl64;
+                if (h.length > KMWS_MAX_FRAME_DATA_LENGTH) {
+                    dec->state = St::IN_ERROR;
+                    result = KMWS_WS_INVALID_LENGTH;
+                    break;
+                }
+            } else {
+                h.length = h.plen;
+            }
+            dec->state = St::MASKEY;
+        }
+            [[fallthrough]];
+        case St::MASKEY: {  // :205-234
+            if (h.mask) {
+                if (dec->mode == KMWS_MODE_CLIENT) {
+                    dec->state = St::IN_ERROR;
+                    result = KMWS_WS_PROTOCOL_ERROR;
+                    break;
+                }
+                size_t c = 4u - dec->pos;
+                if (c > len - p) c = len - p;
+                std::memcpy(h.maskey + dec->pos, data + p, c);
+                p += c;
+                dec->pos = (uint8_t)(dec->pos + c);
+                if (dec->pos < 4) {
+                    result = KMWS_WS_NEED_MORE_DATA;
+                    break;
+                }
+                dec->pos = 0;
+            } else if (dec->mode == KMWS_MODE_SERVER && h.length > 0) {
+                dec->state = St::IN_ERROR;
+                result = KMWS_WS_PROTOCOL_ERROR;
+                break;
+            }
+            dec->buf.clear();
+            dec->state = St::DATA;
+        }
+            [[fallthrough]];
+        case St::DATA: {  // :235-272
+            if (len - p + dec->buf.size() < h.length) {
+                dec->buf.insert(dec->buf.end(), data + p, data + len);
+                p = len;
+                result = KMWS_WS_NEED_MORE_DATA;
+                break;
+            }
+            int st;
+            if (dec->buf.empty()) {  // whole payload in this chunk (:247-250)
+                st = sink(h, data + p, (std::vector<uint8_t>*)nullptr);
+                p += h.length;
+            } else {  // reassembled in ctx_.buf (:251-258)
+                const size_t read_len = h.length - dec->buf.size();
+                dec->buf.insert(dec->buf.end(), data + p, data + p + read_len);
+                p += read_len;
+                st = sink(h, dec->buf.data(), &dec->buf);
+            }
+            if (st != KMWS_OK) return st;
+            if (h.opcode == KMWS_OP_CLOSE) {  // :265-268
+                dec->state = St::CLOSED;
+                result = KMWS_WS_CLOSED;
+                break;
+            }
+            dec->reset_ctx();  // :270
+            break;
+        }
+        default:
+            result = KMWS_WS_INVALID_FRAME;  // :273-276
+            break;
+        }
+    }
+    if (result == kParsing) result = dec->state == St::HDR1 ? KMWS_WS_NOERR : KMWS_WS_NEED_MORE_DATA;  // :279
+    return result;
+}
+
+}  // namespace
+
+extern "C" {
+
+kmws_decoder* kmws_decoder_create(int mode, int device)
+{
+    kmws_decoder* d = new (std::nothrow) kmws_decoder();
+    if (d) {
+        d->mode = mode;
+        d->device = device;
+    }
+    return d;
+}
+
+void kmws_decoder_destroy(kmws_decoder* dec) { delete dec; }
+
+void kmws_decoder_set_mode(kmws_decoder* dec, int mode)
+{
+    if (dec) dec->mode = mode;
+}
+
+void kmws_decoder_reset(kmws_decoder* dec)
+{
+    if (dec) dec->reset_ctx();
+}
+
+// WSHandler::handleData (WSHandler.cpp:41-44, decodeFrame :108-280) in three
+// phases: (1) parse the chunk, collecting completed frames; (2) one GPU unmask
+// batch over their masked payloads -- in place in the caller's chunk when it
+// is pinned memory, else on a pinned staging copy; (3) deliver in order
+// (staged frames that lay in the chunk are first written back there, as the
+// reference unmasks them in place), stopping at a callback that destroyed
+// the decoder.
+int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_cb cb, void* user)
+{
+    if (!dec || (len && !data)) return KMWS_ERR_INVALID_PARAM;
+    dec->pending.clear();
+    dec->held.clear();
+    dec->chunk_descs.clear();
+    dec->stage.clear();
+    int chunk_pinned = -1;  // resolved at the first masked in-chunk frame
+    uint8_t* chunk_base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(data) & ~(uintptr_t)15);
+
+    auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>* reasm) -> int {
+        Pending q{};
+        q.hdr = h;
+        const bool masked = h.mask && h.length;  // handleDataMask is a no-op otherwise (:293, :305)
+        uint32_t key;
+        std::memcpy(&key, h.maskey, 4);
+        if (masked) {
+            kmws_status st = dec->stage.init(dec->device);
+            if (st != KMWS_OK) return st;
+        }
+        if (!reasm) {
+            q.data_ptr = payload;
+            if (!masked) {
+                q.where = kInChunk;
+            } else {
+                if (chunk_pinned < 0) chunk_pinned = device_view(chunk_base) != nullptr;
+                if (chunk_pinned) {
+                    dec->chunk_descs.push_back(kmws_desc{(uint64_t)(payload - chunk_base), h.length, key});
+                    q.where = kInChunkPinned;
+                } else {
+                    kmws_status st = dec->stage.reserve(h.length);
+                    if (st != KMWS_OK) return st;
+                    q.stage_off = dec->stage.append(payload, h.length);
+                    dec->stage.add_desc(q.stage_off, h.length, key);
+                    q.where = kInChunkStaged;
+                }
+            }
+        } else if (masked) {
+            kmws_status st = dec->stage.reserve(h.length);
+            if (st != KMWS_OK) return st;
+            q.stage_off = dec->stage.append(payload, h.length);
+            dec->stage.add_desc(q.stage_off, h.length, key);
+            q.where = kStagedMasked;
+        } else {
+            dec->held.emplace_back();
+            dec->held.back().swap(*reasm);
+            q.hold_idx = dec->held.size() - 1;
+            q.where = kHeld;
+        }
+        dec->pending.push_back(q);
+        return KMWS_OK;
+    };
+
+    const int result = parse_chunk(dec, data, len, sink);
+    if (result < 0) return result;
+
+    // ---- GPU unmask of every masked payload of this call ----
+    if (dec->stage.n_desc() || !dec->chunk_descs.empty()) {
+        const uint64_t chunk_span = (uint64_t)((data + len) - chunk_base);
+        kmws_status st = dec->stage.run(chunk_base, chunk_span, &dec->chunk_descs);
+        if (st != KMWS_OK) return st;
+    }
+
+    // ---- in-order delivery ----
+    std::vector<Pending> todo;
+    todo.swap(dec->pending);
+    std::vector<std::vector<uint8_t>> held;
+    held.swap(dec->held);
+    uint8_t* stage = dec->stage.data();
+    for (Pending& q : todo) {
+        uint8_t* payload;
+        switch (q.where) {
+        case kInChunkStaged:  // unmasked in place in the caller's buffer, as kuma does (:260)
+            std::memcpy(q.data_ptr, stage + q.stage_off, q.hdr.length);
+            payload = q.data_ptr;
+            break;
+        case kStagedMasked: payload = stage + q.stage_off; break;
+        case kHeld: payload = held[q.hold_idx].data(); break;
+        default: payload = q.data_ptr; break;  // kInChunk, kInChunkPinned
+        }
+        // WSHandler::handleFrame (:282-289): a callback that destroyed its
+        // owner ends the call; the decoder must not be touched afterwards.
+        if (cb && cb(&q.hdr, payload, q.hdr.length, user)) return KMWS_WS_DESTROYED;
+    }
+    return result;
+}
+
+// ---- deferred delivery across calls and connections ----
+
+kmws_rx_batch* kmws_rx_batch_create(int device)
+{
+    kmws_rx_batch* b = new (std::nothrow) kmws_rx_batch();
+    if (!b) return nullptr;
+    b->device = device;
+    if (b->stage.init(device) != KMWS_OK) {
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+void kmws_rx_batch_destroy(kmws_rx_batch* b) { delete b; }
+
+int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_t* data, size_t len,
+                               kmws_frame_cb cb, void* user)
+{
+    if (!dec || !b || (len && !data)) return KMWS_ERR_INVALID_PARAM;
+    if (b->flushing) return KMWS_ERR_INVALID_STATE;
+    // The chunk does not outlive this call (kuma reads into a stack buffer,
+    // TcpConnection.cpp:229), so every payload is copied into the batch.  The
+    // parse does not write into the chunk.
+    auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>*) -> int {
+        kmws_status st = b->stage.reserve(h.length);
+        if (st != KMWS_OK) return st;
+        const size_t off = b->stage.append(payload, h.length);
+        if (h.mask && h.length) {
+            uint32_t key;
+            std::memcpy(&key, h.maskey, 4);
+            b->stage.add_desc(off, h.length, key);
+        }
+        b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off});
+        return KMWS_OK;
+    };
+    return parse_chunk(dec, const_cast<uint8_t*>(data), len, sink);
+}
+
+int kmws_rx_batch_pending(const kmws_rx_batch* b) { return b ? (int)b->items.size() : 0; }
+
+void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
+{
+    if (!b) return;
+    for (auto& it : b->items)
+        if (it.dec == dec) it.dec = nullptr, it.cb = nullptr;
+}
+
+int kmws_rx_batch_flush(kmws_rx_batch* b)
+{
+    if (!b) return KMWS_ERR_INVALID_PARAM;
+    if (b->flushing) return KMWS_ERR_INVALID_STATE;
+    kmws_status st = b->stage.run();
+    if (st != KMWS_OK) return st;
+    std::vector<kmws_rx_batch::Item> items;
+    items.swap(b->items);
+    int delivered = 0;
+    std::vector<const kmws_decoder*> destroyed;
+    b->flushing = true;
+    for (auto& it : items) {
+        if (!it.cb) continue;
+        bool dead = false;
+        for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
+        if (dead) continue;
+        ++delivered;
+        if (it.cb(&it.hdr, b->stage.data() + it.off, it.hdr.length, it.user)) destroyed.push_back(it.dec);
+    }
+    b->flushing = false;
+    b->stage.clear();
+    return delivered;
+}
+
+}  // extern "C"

@@ -35,6 +35,8 @@ EXPORTS = [
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
+    "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
+    "kmws_rx_batch_pending", "kmws_rx_batch_discard",
 ]
 
 
@@ -104,6 +106,12 @@ def lib() -> C.CDLL:
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
         "kmws_pipeline_destroy": (None, [vp]),
+        "kmws_rx_batch_create": (vp, [i32]),
+        "kmws_rx_batch_destroy": (None, [vp]),
+        "kmws_decoder_feed_deferred": (i32, [vp, vp, u8p, sz, FRAME_CB, vp]),
+        "kmws_rx_batch_flush": (i32, [vp]),
+        "kmws_rx_batch_pending": (i32, [vp]),
+        "kmws_rx_batch_discard": (None, [vp, vp]),
         "kmws_pipeline_set_transfer": (i32, [vp, i32]),
         "kmws_pipeline_unmask": (i32, [vp, u8p, u64, vp, u32]),
         "kmws_find_headers": (i32, [u8p, u64, vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
@@ -214,7 +222,46 @@ class WSHandler:
             buf = (C.c_uint8 * max(1, n)).from_buffer_copy(bytes(data) if n else b"\0")
         return lib().kmws_decoder_feed(self._d, buf, n, self._tramp, None)
 
+    def handleDataPtr(self, ptr: int, n: int) -> int:
+        """Feed raw memory (e.g. a pinned torch CPU tensor's data_ptr()) in place."""
+        return lib().kmws_decoder_feed(self._d, ptr, n, self._tramp, None)
+
+    def handleDataDeferred(self, batch: "RxBatch", data) -> int:
+        """kmws_decoder_feed_deferred: parse now, deliver at batch.flush()."""
+        n = len(data)
+        buf = (C.c_uint8 * max(1, n)).from_buffer_copy(bytes(data) if n else b"\0")
+        return lib().kmws_decoder_feed_deferred(self._d, batch._b, buf, n, self._tramp, None)
+
     encodeFrameHeader = staticmethod(encode_frame_header)
+
+
+class RxBatch:
+    """kmws_rx_batch: one GPU unmask per flush for frames of many feeds/connections."""
+
+    def __init__(self, device: int = 0):
+        self._b = lib().kmws_rx_batch_create(device)
+        if not self._b:
+            raise RuntimeError("kmws_rx_batch_create failed (no gfx950 device)")
+
+    def flush(self) -> int:
+        r = lib().kmws_rx_batch_flush(self._b)
+        if r < 0:
+            raise RuntimeError(f"kmws_rx_batch_flush: {r}")
+        return r
+
+    def pending(self) -> int:
+        return lib().kmws_rx_batch_pending(self._b)
+
+    def discard(self, handler: WSHandler) -> None:
+        lib().kmws_rx_batch_discard(self._b, handler._d)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_b", None):
+                lib().kmws_rx_batch_destroy(self._b)
+                self._b = None
+        except Exception:
+            pass
 
 
 # ====================== device batch entries (torch tensors) ======================

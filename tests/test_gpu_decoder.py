@@ -123,3 +123,75 @@ def test_callback_destroy_stops_delivery():
     h.setFrameCallback(cb)
     assert h.handleData(stream) == r_o == kmws.WS_DESTROYED
     assert got == [f.key() for f in d.frames]
+
+
+@pytest.mark.parametrize("chunk", [0, 4096, 65536])
+def test_pinned_chunk_unmasked_in_place(chunk):
+    """Caller's receive buffer in pinned memory: the kernel unmasks it in place
+    (zero-copy); callbacks and the buffer's bytes match the oracle."""
+    import torch
+    stream = masked_stream(1000 + chunk, 60)
+    want_rets, want_frames, want_buf = run_oracle(stream, orc.SERVER, chunk, inplace=True)
+    h = kmws.WSHandler(kmws.SERVER)
+    got = []
+    h.setFrameCallback(lambda hd, p: got.append(frame_key(hd, p)))
+    step = chunk if chunk > 0 else len(stream)
+    rets, bufs = [], []
+    for i in range(0, len(stream), step):
+        piece = torch.frombuffer(bytearray(stream[i:i + step]), dtype=torch.uint8).pin_memory()
+        rets.append(h.handleDataPtr(piece.data_ptr(), piece.numel()))
+        bufs.append(bytes(piece.numpy()))
+    assert rets == want_rets
+    assert got == want_frames
+    assert b"".join(bufs) == want_buf
+
+
+def test_deferred_batch_many_connections():
+    """Interleaved reads of several connections fed deferred, one flush per
+    'loop iteration': per-connection callbacks and return codes == oracle."""
+    nconn, chunk = 5, 3000
+    streams = [masked_stream(500 + c, 25) for c in range(nconn)]
+    want = [run_oracle(s, orc.SERVER, chunk) for s in streams]
+    batch = kmws.RxBatch(0)
+    hs, got, rets = [], [[] for _ in range(nconn)], [[] for _ in range(nconn)]
+    for c in range(nconn):
+        h = kmws.WSHandler(kmws.SERVER)
+        h.setFrameCallback(lambda hd, p, c=c: got[c].append(frame_key(hd, p)))
+        hs.append(h)
+    pos = [0] * nconn
+    it = 0
+    while any(pos[c] < len(streams[c]) for c in range(nconn)):
+        for c in range(nconn):
+            if pos[c] < len(streams[c]):
+                rets[c].append(hs[c].handleDataDeferred(batch, streams[c][pos[c]:pos[c] + chunk]))
+                pos[c] += chunk
+        it += 1
+        if it % 3 == 0:  # several reads per loop iteration
+            batch.flush()
+    batch.flush()
+    assert batch.pending() == 0
+    for c in range(nconn):
+        assert rets[c] == want[c][0]
+        assert got[c] == want[c][1]
+
+
+def test_deferred_destroy_drops_only_that_connection():
+    a_stream, b_stream = masked_stream(71, 10, sizes=(5, 300)), masked_stream(72, 10, sizes=(7, 200))
+    batch = kmws.RxBatch(0)
+    ha, hb = kmws.WSHandler(kmws.SERVER), kmws.WSHandler(kmws.SERVER)
+    ga, gb = [], []
+
+    def cba(hd, p):
+        ga.append(p)
+        return len(ga) == 2  # "destroyed" after its 2nd frame
+
+    ha.setFrameCallback(cba)
+    hb.setFrameCallback(lambda hd, p: gb.append(p))
+    ha.handleDataDeferred(batch, a_stream)
+    hb.handleDataDeferred(batch, b_stream)
+    n = batch.flush()
+    _, fb, _ = run_oracle(b_stream, orc.SERVER, 0)
+    _, fa, _ = run_oracle(a_stream, orc.SERVER, 0)
+    assert ga == [f[-1] for f in fa[:2]]
+    assert gb == [f[-1] for f in fb]
+    assert n == 2 + len(fb)
