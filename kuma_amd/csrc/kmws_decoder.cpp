@@ -80,6 +80,7 @@ struct kmws_rx_batch {
         void* user;
         kmws_frame_hdr hdr;
         size_t off;
+        bool live;  // false once discarded
     };
     PinnedStage stage;
     std::vector<Item> items;
@@ -396,7 +397,7 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
             std::memcpy(&key, h.maskey, 4);
             b->stage.add_desc(off, h.length, key);
         }
-        b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off});
+        b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off, true});
         return KMWS_OK;
     };
     return parse_chunk(dec, const_cast<uint8_t*>(data), len, sink);
@@ -408,7 +409,7 @@ void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
 {
     if (!b) return;
     for (auto& it : b->items)
-        if (it.dec == dec) it.dec = nullptr, it.cb = nullptr;
+        if (it.dec == dec) it.live = false;
 }
 
 int kmws_rx_batch_flush(kmws_rx_batch* b)
@@ -423,12 +424,12 @@ int kmws_rx_batch_flush(kmws_rx_batch* b)
     std::vector<const kmws_decoder*> destroyed;
     b->flushing = true;
     for (auto& it : items) {
-        if (!it.cb) continue;
+        if (!it.live) continue;
         bool dead = false;
         for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
         if (dead) continue;
-        ++delivered;
-        if (it.cb(&it.hdr, b->stage.data() + it.off, it.hdr.length, it.user)) destroyed.push_back(it.dec);
+        ++delivered;  // a NULL callback consumes the frame, like WSHandler without frame_cb_ (:286)
+        if (it.cb && it.cb(&it.hdr, b->stage.data() + it.off, it.hdr.length, it.user)) destroyed.push_back(it.dec);
     }
     b->flushing = false;
     b->stage.clear();
