@@ -114,6 +114,14 @@ void          kmws_decoder_reset(kmws_decoder* dec);                /* WSHandler
  * failed. */
 int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_cb cb, void* user);
 
+/* WSHandler::handleDataMask(key, KMBuffer&) (WSHandler.cpp:312-322) and, with
+ * nseg == 1, handleDataMask(key, data, len) (:303-310) for HOST buffers: the
+ * segments of a chain are masked in place with the key phase continuing
+ * across segments.  Runs on the GPU (gathered into pinned staging, one
+ * unmask launch, scattered back); synchronous; per-thread staging. */
+kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t* const* segs, const size_t* lens,
+                                 size_t nseg, int device);
+
 /* ---- deferred delivery: one GPU batch per event-loop iteration (SURVEY f-1) ----
  * kuma calls handleData once per 64 KiB socket read per connection; a GPU
  * round trip per call costs more than the scalar unmask it replaces.  A loop

@@ -364,6 +364,69 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     return result;
 }
 
+// ---- host-buffer masking: WSHandler::handleDataMask statics (a-1, a-2) ----
+
+namespace {
+struct TxStages {  // one staging area per device, for the synchronous host mask entries
+    std::vector<PinnedStage*> by_dev;
+    ~TxStages()
+    {
+        for (PinnedStage* s : by_dev) delete s;
+    }
+};
+PinnedStage* tx_stage(int device)
+{
+    static thread_local TxStages t;  // objects are per loop thread, like kuma's (README.md:15)
+    if (device < 0) return nullptr;
+    if ((size_t)device >= t.by_dev.size()) t.by_dev.resize(device + 1, nullptr);
+    if (!t.by_dev[device]) t.by_dev[device] = new (std::nothrow) PinnedStage();
+    return t.by_dev[device];
+}
+}  // namespace
+
+// Masks a chain of host segments in place with the key phase continuing across
+// segments (WSHandler.cpp:312-322; one segment = :303-310).  The segments are
+// gathered back to back into pinned staging -- so the chain is one payload and
+// one descriptor -- unmasked by the GPU in place there, and scattered back.
+kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t* const* segs, const size_t* lens,
+                                 size_t nseg, int device)
+{
+    if (!key || (nseg && (!segs || !lens))) return KMWS_ERR_INVALID_PARAM;
+    size_t total = 0;
+    for (size_t i = 0; i < nseg; ++i) {
+        if (lens[i] && !segs[i]) return KMWS_ERR_INVALID_PARAM;
+        total += lens[i];
+    }
+    if (total == 0) return KMWS_OK;  // nothing to do (:305)
+    if (total > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    PinnedStage* s = tx_stage(device);
+    if (!s) return KMWS_ERR_INVALID_PARAM;
+    kmws_status st = s->init(device);
+    if (st != KMWS_OK) return st;
+    s->clear();
+    st = s->reserve(total);
+    if (st != KMWS_OK) return st;
+    size_t off = 0;
+    uint8_t* dst = s->alloc(total, &off);
+    size_t pos = 0;
+    for (size_t i = 0; i < nseg; ++i) {
+        if (lens[i]) std::memcpy(dst + pos, segs[i], lens[i]);
+        pos += lens[i];
+    }
+    uint32_t k;
+    std::memcpy(&k, key, 4);
+    s->add_desc(off, (uint32_t)total, k);
+    st = s->run();
+    if (st != KMWS_OK) return st;
+    pos = 0;
+    for (size_t i = 0; i < nseg; ++i) {
+        if (lens[i]) std::memcpy(segs[i], dst + pos, lens[i]);
+        pos += lens[i];
+    }
+    s->clear();
+    return KMWS_OK;
+}
+
 // ---- deferred delivery across calls and connections ----
 
 kmws_rx_batch* kmws_rx_batch_create(int device)

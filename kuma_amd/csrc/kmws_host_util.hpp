@@ -102,6 +102,13 @@ public:
         len_ = off + n;
         return off;
     }
+    // Room for n bytes at a 16-B aligned offset (after reserve(n)); the caller fills it.
+    uint8_t* alloc(size_t n, size_t* off)
+    {
+        *off = (len_ + 15) & ~(size_t)15;
+        len_ = *off + n;
+        return h_ + *off;
+    }
     uint8_t* data() { return h_; }
     void add_desc(uint64_t off, uint32_t len, uint32_t key) { descs_.push_back(kmws_desc{off, len, key}); }
     size_t n_desc() const { return descs_.size(); }

@@ -36,7 +36,7 @@ EXPORTS = [
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
-    "kmws_rx_batch_pending", "kmws_rx_batch_discard",
+    "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
 ]
 
 
@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
         "kmws_pipeline_destroy": (None, [vp]),
+        "kmws_mask_host_chain": (i32, [vp, vp, vp, sz, i32]),
         "kmws_rx_batch_create": (vp, [i32]),
         "kmws_rx_batch_destroy": (None, [vp]),
         "kmws_decoder_feed_deferred": (i32, [vp, vp, u8p, sz, FRAME_CB, vp]),
@@ -233,6 +234,16 @@ class WSHandler:
         return lib().kmws_decoder_feed_deferred(self._d, batch._b, buf, n, self._tramp, None)
 
     encodeFrameHeader = staticmethod(encode_frame_header)
+
+
+def handle_data_mask(key: bytes, segments, device: int = 0) -> None:
+    """WSHandler::handleDataMask over a chain of bytearrays (in place, GPU)."""
+    segs = list(segments)
+    bufs = [(C.c_uint8 * max(1, len(s))).from_buffer(s) if len(s) else (C.c_uint8 * 1)() for s in segs]
+    ptrs = (C.c_void_p * max(1, len(segs)))(*[C.addressof(b) for b in bufs])
+    lens = (C.c_size_t * max(1, len(segs)))(*[len(s) for s in segs])
+    k = (C.c_uint8 * 4).from_buffer_copy(bytes(key))
+    _check(lib().kmws_mask_host_chain(k, ptrs, lens, len(segs), device), "kmws_mask_host_chain")
 
 
 class RxBatch:

@@ -195,3 +195,22 @@ def test_deferred_destroy_drops_only_that_connection():
     assert ga == [f[-1] for f in fa[:2]]
     assert gb == [f[-1] for f in fb]
     assert n == 2 + len(fb)
+
+
+def test_mask_host_chain_golden_and_random():
+    """handleDataMask(key, KMBuffer&) over host segments: phase continues across
+    segments (SURVEY a-2 vector) and equals the oracle's chain mask."""
+    import json as _json
+    gold = _json.load(open(os.path.join(ROOT, "tests", "golden", "reference_vectors.json")))
+    for c in gold["mask"]:
+        segs = [bytearray.fromhex(s) for s in c["segments_hex"]]
+        kmws.handle_data_mask(bytes.fromhex(c["key"]), segs)
+        assert [s.hex() for s in segs] == c["expect_hex"], c["name"]
+    rng = random.Random(5)
+    for _ in range(20):
+        segs = [bytearray(rng.randrange(256) for _ in range(rng.choice([0, 1, 3, 5, 17, 1000, 70000])))
+                for _ in range(rng.randrange(1, 6))]
+        key = bytes(rng.randrange(256) for _ in range(4))
+        want = orc.mask_chain(key, [bytes(s) for s in segs])
+        kmws.handle_data_mask(key, segs)
+        assert [bytes(s) for s in segs] == want
