@@ -367,20 +367,16 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
 // ---- host-buffer masking: WSHandler::handleDataMask statics (a-1, a-2) ----
 
 namespace {
-struct TxStages {  // one staging area per device, for the synchronous host mask entries
-    std::vector<PinnedStage*> by_dev;
-    ~TxStages()
-    {
-        for (PinnedStage* s : by_dev) delete s;
-    }
-};
+// One staging area per device and loop thread for the synchronous host mask
+// entry.  Never freed: releasing pinned memory from a thread_local destructor
+// can run after the HIP runtime has been torn down at process exit.
 PinnedStage* tx_stage(int device)
 {
-    static thread_local TxStages t;  // objects are per loop thread, like kuma's (README.md:15)
+    static thread_local std::vector<PinnedStage*>* by_dev = new std::vector<PinnedStage*>();
     if (device < 0) return nullptr;
-    if ((size_t)device >= t.by_dev.size()) t.by_dev.resize(device + 1, nullptr);
-    if (!t.by_dev[device]) t.by_dev[device] = new (std::nothrow) PinnedStage();
-    return t.by_dev[device];
+    if ((size_t)device >= by_dev->size()) by_dev->resize(device + 1, nullptr);
+    if (!(*by_dev)[device]) (*by_dev)[device] = new (std::nothrow) PinnedStage();
+    return (*by_dev)[device];
 }
 }  // namespace
 
