@@ -142,6 +142,12 @@ int            kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, c
                                           kmws_frame_cb cb, void* user);
 int            kmws_rx_batch_flush(kmws_rx_batch* b);  /* frames delivered, or negative status */
 int            kmws_rx_batch_pending(const kmws_rx_batch* b);
+/* Optional pinned receive ring (hipHostMalloc / hipHostRegister) that the loop
+ * reads sockets into: chunks fed from inside it are not copied -- their
+ * masked payloads are unmasked in place there at flush (zero-copy), and the
+ * callback views point into the ring.  The ring bytes fed since the last
+ * flush must stay unmodified until that flush.  NULL detaches. */
+kmws_status    kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes);
 void           kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec);
 
 /* ======================= device batch entries ======================= */

@@ -79,11 +79,15 @@ struct kmws_rx_batch {
         kmws_frame_cb cb;
         void* user;
         kmws_frame_hdr hdr;
-        size_t off;
-        bool live;  // false once discarded
+        size_t off;       // payload offset in the staging area (direct == nullptr)
+        uint8_t* direct;  // payload in the attached ring (no copy)
+        bool live;        // false once discarded
     };
     PinnedStage stage;
     std::vector<Item> items;
+    uint8_t* ring = nullptr;  // caller's pinned receive ring (optional)
+    size_t ring_bytes = 0;
+    std::vector<kmws_desc> ring_descs;
     int device = 0;
     bool flushing = false;  // feeding the batch from inside its own flush is refused
 };
@@ -447,19 +451,33 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
     // The chunk does not outlive this call (kuma reads into a stack buffer,
     // TcpConnection.cpp:229), so every payload is copied into the batch.  The
     // parse does not write into the chunk.
-    auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>*) -> int {
+    auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>* reasm) -> int {
+        uint32_t key;
+        std::memcpy(&key, h.maskey, 4);
+        const bool masked = h.mask && h.length;
+        if (!reasm && b->ring && payload >= b->ring && payload + h.length <= b->ring + b->ring_bytes) {
+            // payload lies in the caller's pinned ring: unmasked there at flush, no copy
+            if (masked) b->ring_descs.push_back(kmws_desc{(uint64_t)(payload - b->ring), h.length, key});
+            b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, 0, payload, true});
+            return KMWS_OK;
+        }
         kmws_status st = b->stage.reserve(h.length);
         if (st != KMWS_OK) return st;
         const size_t off = b->stage.append(payload, h.length);
-        if (h.mask && h.length) {
-            uint32_t key;
-            std::memcpy(&key, h.maskey, 4);
-            b->stage.add_desc(off, h.length, key);
-        }
-        b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off, true});
+        if (masked) b->stage.add_desc(off, h.length, key);
+        b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off, nullptr, true});
         return KMWS_OK;
     };
     return parse_chunk(dec, const_cast<uint8_t*>(data), len, sink);
+}
+
+kmws_status kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes)
+{
+    if (!b || b->flushing || !b->items.empty()) return KMWS_ERR_INVALID_STATE;
+    if (ring && (!bytes || !device_view(ring))) return KMWS_ERR_INVALID_PARAM;  // must be pinned
+    b->ring = ring;
+    b->ring_bytes = ring ? bytes : 0;
+    return KMWS_OK;
 }
 
 int kmws_rx_batch_pending(const kmws_rx_batch* b) { return b ? (int)b->items.size() : 0; }
@@ -475,7 +493,7 @@ int kmws_rx_batch_flush(kmws_rx_batch* b)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
     if (b->flushing) return KMWS_ERR_INVALID_STATE;
-    kmws_status st = b->stage.run();
+    kmws_status st = b->stage.run(b->ring, b->ring_bytes, &b->ring_descs);
     if (st != KMWS_OK) return st;
     std::vector<kmws_rx_batch::Item> items;
     items.swap(b->items);
@@ -488,10 +506,12 @@ int kmws_rx_batch_flush(kmws_rx_batch* b)
         for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
         if (dead) continue;
         ++delivered;  // a NULL callback consumes the frame, like WSHandler without frame_cb_ (:286)
-        if (it.cb && it.cb(&it.hdr, b->stage.data() + it.off, it.hdr.length, it.user)) destroyed.push_back(it.dec);
+        uint8_t* payload = it.direct ? it.direct : b->stage.data() + it.off;
+        if (it.cb && it.cb(&it.hdr, payload, it.hdr.length, it.user)) destroyed.push_back(it.dec);
     }
     b->flushing = false;
     b->stage.clear();
+    b->ring_descs.clear();
     return delivered;
 }
 

@@ -130,8 +130,8 @@ public:
         if (st != KMWS_OK) return st;
         std::memcpy(h_desc_, descs_.data(), n1 * sizeof(kmws_desc));
         if (n2) std::memcpy(h_desc_ + n1, extra->data(), n2 * sizeof(kmws_desc));
-        if (hipMemcpyAsync(d_desc_, h_desc_, (n1 + n2) * sizeof(kmws_desc), hipMemcpyHostToDevice, stream_) !=
-            hipSuccess)
+        if (n1 && hipMemcpyAsync(d_desc_, h_desc_, n1 * sizeof(kmws_desc), hipMemcpyHostToDevice, stream_) !=
+                      hipSuccess)
             return KMWS_ERR_FAILED;
         uint32_t status[2] = {0, 0};
         if (n1) {
@@ -143,9 +143,22 @@ public:
                 return KMWS_ERR_FAILED;
         }
         if (n2) {
+            // Only the extent the descriptors cover is processed: rebase them
+            // onto its 16-B aligned start (a large pinned ring may hold few frames).
+            uint64_t lo = ~0ull, hi = 0;
+            for (const kmws_desc& x : *extra) {
+                lo = std::min<uint64_t>(lo, x.off);
+                hi = std::max<uint64_t>(hi, x.off + x.len);
+            }
+            lo &= ~(uint64_t)15;
+            if (hi > extra_span) return KMWS_ERR_INVALID_PARAM;
+            for (size_t i = 0; i < n2; ++i) h_desc_[n1 + i].off -= lo;
+            if (hipMemcpyAsync(d_desc_ + n1, h_desc_ + n1, n2 * sizeof(kmws_desc), hipMemcpyHostToDevice, stream_) !=
+                hipSuccess)
+                return KMWS_ERR_FAILED;
             uint8_t* dv = static_cast<uint8_t*>(device_view(extra_base));
             if (!dv) return KMWS_ERR_INVALID_PARAM;
-            st = kmws_unmask_batch(dv, extra_span, d_desc_ + n1, (uint32_t)n2, d_ws_[1], ws_cap_, stream_);
+            st = kmws_unmask_batch(dv + lo, hi - lo, d_desc_ + n1, (uint32_t)n2, d_ws_[1], ws_cap_, stream_);
             if (st != KMWS_OK) return st;
             if (hipMemcpyAsync(&status[1], d_ws_[1], 4, hipMemcpyDeviceToHost, stream_) != hipSuccess)
                 return KMWS_ERR_FAILED;

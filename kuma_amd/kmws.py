@@ -37,6 +37,7 @@ EXPORTS = [
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
+    "kmws_rx_batch_attach_ring",
 ]
 
 
@@ -111,6 +112,7 @@ def lib() -> C.CDLL:
         "kmws_rx_batch_destroy": (None, [vp]),
         "kmws_decoder_feed_deferred": (i32, [vp, vp, u8p, sz, FRAME_CB, vp]),
         "kmws_rx_batch_flush": (i32, [vp]),
+        "kmws_rx_batch_attach_ring": (i32, [vp, vp, sz]),
         "kmws_rx_batch_pending": (i32, [vp]),
         "kmws_rx_batch_discard": (None, [vp, vp]),
         "kmws_pipeline_set_transfer": (i32, [vp, i32]),
@@ -227,6 +229,10 @@ class WSHandler:
         """Feed raw memory (e.g. a pinned torch CPU tensor's data_ptr()) in place."""
         return lib().kmws_decoder_feed(self._d, ptr, n, self._tramp, None)
 
+    def handleDataDeferredPtr(self, batch: "RxBatch", ptr: int, n: int) -> int:
+        """Deferred feed of raw memory (e.g. a slice of a ring attached to `batch`)."""
+        return lib().kmws_decoder_feed_deferred(self._d, batch._b, ptr, n, self._tramp, None)
+
     def handleDataDeferred(self, batch: "RxBatch", data) -> int:
         """kmws_decoder_feed_deferred: parse now, deliver at batch.flush()."""
         n = len(data)
@@ -262,6 +268,13 @@ class RxBatch:
 
     def pending(self) -> int:
         return lib().kmws_rx_batch_pending(self._b)
+
+    def attach_ring(self, ring) -> None:
+        """ring: pinned torch uint8 CPU tensor (kept alive by this object)."""
+        self._ring = ring
+        _check(lib().kmws_rx_batch_attach_ring(self._b, ring.data_ptr() if ring is not None else None,
+                                               ring.numel() if ring is not None else 0),
+               "kmws_rx_batch_attach_ring")
 
     def discard(self, handler: WSHandler) -> None:
         lib().kmws_rx_batch_discard(self._b, handler._d)

@@ -214,3 +214,38 @@ def test_mask_host_chain_golden_and_random():
         want = orc.mask_chain(key, [bytes(s) for s in segs])
         kmws.handle_data_mask(key, segs)
         assert [bytes(s) for s in segs] == want
+
+
+def test_deferred_ring_zero_copy():
+    """Reads placed in an attached pinned ring are unmasked in place at flush;
+    callbacks == oracle, frames reassembled across reads still correct."""
+    import torch
+    nconn, chunk = 3, 5000
+    streams = [masked_stream(900 + c, 20) for c in range(nconn)]
+    want = [run_oracle(s, orc.SERVER, chunk) for s in streams]
+    ring = torch.zeros(1 << 20, dtype=torch.uint8).pin_memory()
+    batch = kmws.RxBatch(0)
+    batch.attach_ring(ring)
+    hs, got, rets = [], [[] for _ in range(nconn)], [[] for _ in range(nconn)]
+    for c in range(nconn):
+        h = kmws.WSHandler(kmws.SERVER)
+        h.setFrameCallback(lambda hd, p, c=c: got[c].append(frame_key(hd, p)))
+        hs.append(h)
+    pos, wr = [0] * nconn, 0
+    base = ring.data_ptr()
+    while any(pos[c] < len(streams[c]) for c in range(nconn)):
+        for c in range(nconn):
+            piece = streams[c][pos[c]:pos[c] + chunk]
+            if not piece:
+                continue
+            if wr + len(piece) > ring.numel():  # ring full: flush, then wrap
+                batch.flush()
+                wr = 0
+            ring[wr:wr + len(piece)] = torch.frombuffer(bytearray(piece), dtype=torch.uint8)
+            rets[c].append(hs[c].handleDataDeferredPtr(batch, base + wr, len(piece)))
+            wr += len(piece) + 7  # leave gaps like unaligned socket reads
+            pos[c] += chunk
+    batch.flush()
+    for c in range(nconn):
+        assert rets[c] == want[c][0]
+        assert got[c] == want[c][1]
