@@ -179,7 +179,8 @@ kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, 
 kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                               const void* workspace, size_t workspace_bytes, void* stream);
 
-/* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2). */
+/* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2);
+ * 16 KiB tiles on a persistent grid-stride grid of 4096 (3), 6144 (4) or 8192 (5) blocks. */
 kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       void* workspace, size_t workspace_bytes, void* stream, int variant);
 

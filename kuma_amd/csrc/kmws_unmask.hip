@@ -49,35 +49,30 @@ __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __res
     for (uint64_t b = b0; b < b1; ++b) map[b] = f;
 }
 
+// Issue every payload load of a tile.  Full tiles load unconditionally so the
+// loads stay back to back.  Payload is touched once: non-temporal loads and
+// stores (measured +6 % on MI355X for this in-place stream, tools/membw_probe.hip).
 template <int V, bool FULL>
-__device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
-                                            const kmws_desc* __restrict__ d, uint32_t n,
-                                            const uint32_t* __restrict__ map, uint32_t tile,
-                                            const WsHead* __restrict__ head,
-                                            uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
+__device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
+                                          u32x4 (&v)[V])
 {
-    using Cfg = UnmaskCfg<V>;
     const int tid = threadIdx.x;
-
-    // 1) Issue every payload load of this lane before any metadata work.
-    //    Full tiles load unconditionally so the loads stay back to back.
-    //    Payload is touched once: non-temporal loads/stores (measured +6%
-    //    on MI355X for this in-place stream, tools/membw_probe.hip).
-    u32x4 v[V];
-    u32x4 m[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
         if (FULL || a < tile_hi) v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + a));
         else v[i] = u32x4{0, 0, 0, 0};
-        m[i] = u32x4{0, 0, 0, 0};
     }
-    // Metadata comes after the payload loads.  No early exit sits between the
-    // loads and their uses, so the compiler cannot sink the loads below the
-    // scalar metadata waits.  A bad plan (status != 0) stores nothing.
-    __builtin_amdgcn_sched_barrier(0);
-    const bool ok = head->status == 0;
-    uint32_t f = map[tile];
+}
+
+// Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
+template <int V, bool FULL>
+__device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
+                                            const kmws_desc* __restrict__ d, uint32_t n, uint32_t f, bool ok,
+                                            const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
+{
+    using Cfg = UnmaskCfg<V>;
+    const int tid = threadIdx.x;
 
     // Fast path: one frame covers the whole tile (every tile of a 64 KiB-frame
     // arena).  The test reads block-uniform scalars only, so the branch is
@@ -93,7 +88,11 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
         return;
     }
 
-    // 2) Stage the descriptors of frames overlapping the tile, kCap per round.
+    // General path: stage the descriptors of frames overlapping the tile in
+    // LDS, kCap per round, and build a byte-exact mask per 16-byte word.
+    u32x4 m[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) m[i] = u32x4{0, 0, 0, 0};
     for (;;) {
         const uint32_t fi = f + (uint32_t)tid;
         int valid = 0;
@@ -108,8 +107,6 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
             }
         }
         const int cnt = __syncthreads_count(valid);  // sorted => a prefix
-
-        // 3) Per-word mask from the staged frames.
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
@@ -135,12 +132,10 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
                 }
             }
         }
+        __syncthreads();  // every lane done reading this round's LDS (also before a next tile reuses it)
         if (cnt < Cfg::kCap) break;
         f += Cfg::kCap;
-        __syncthreads();  // every lane done reading this round's LDS
     }
-
-    // 4) XOR and store the words that carry payload bytes.
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
@@ -150,6 +145,7 @@ __device__ __forceinline__ void unmask_tile(uint8_t* __restrict__ base, uint64_t
     }
 }
 
+// One block per tile.
 template <int V>
 __global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
@@ -160,13 +156,53 @@ __global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restric
     __shared__ uint64_t s_off[Cfg::kCap];
     __shared__ uint64_t s_end[Cfg::kCap];
     __shared__ uint32_t s_key[Cfg::kCap];
-
     const uint32_t tile = tile_base + blockIdx.x;
     const uint64_t tile_lo = (uint64_t)tile * Cfg::kTile;
-    if (tile_lo + Cfg::kTile <= span)
-        unmask_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head, s_off, s_end, s_key);
-    else
-        unmask_tile<V, false>(base, tile_lo, span, d, n, map, tile, head, s_off, s_end, s_key);
+    u32x4 v[V];
+    // Metadata comes after the payload loads, with no early exit between the
+    // loads and their uses, so the compiler cannot sink the loads below the
+    // scalar metadata waits.  A bad plan (status != 0) stores nothing.
+    if (tile_lo + Cfg::kTile <= span) {
+        load_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, v);
+        __builtin_amdgcn_sched_barrier(0);
+        finish_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map[tile], head->status == 0, v, s_off,
+                             s_end, s_key);
+    } else {
+        load_tile<V, false>(base, tile_lo, span, v);
+        __builtin_amdgcn_sched_barrier(0);
+        finish_tile<V, false>(base, tile_lo, span, d, n, map[tile], head->status == 0, v, s_off, s_end, s_key);
+    }
+}
+
+// Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
+// and issues the next tile's loads before finishing the current one.
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_persist_kernel(uint8_t* __restrict__ base,
+                                                                const kmws_desc* __restrict__ d, uint32_t n,
+                                                                const uint32_t* __restrict__ map,
+                                                                const WsHead* __restrict__ head, uint32_t nfull)
+{
+    using Cfg = UnmaskCfg<V>;
+    __shared__ uint64_t s_off[Cfg::kCap];
+    __shared__ uint64_t s_end[Cfg::kCap];
+    __shared__ uint32_t s_key[Cfg::kCap];
+    uint32_t t = blockIdx.x;
+    if (t >= nfull) return;
+    const bool ok = head->status == 0;
+    u32x4 v[V];
+    load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, v);
+    for (;;) {
+        const uint32_t tn = t + gridDim.x;
+        u32x4 w[V];
+        if (tn < nfull) load_tile<V, true>(base, (uint64_t)tn * Cfg::kTile, 0, w);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t lo = (uint64_t)t * Cfg::kTile;
+        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[t], ok, v, s_off, s_end, s_key);
+        if (tn >= nfull) break;
+#pragma unroll
+        for (int i = 0; i < V; ++i) v[i] = w[i];
+        t = tn;
+    }
 }
 
 // ---- synthetic fill: byte i = byte (i & 7) of splitmix64(seed + (i >> 3)) ----
@@ -295,6 +331,30 @@ static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* d
 }
 
 template <int V>
+static kmws_status launch_apply_persist(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                        const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t grid)
+{
+    using Cfg = UnmaskCfg<V>;
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    if (n == 0 || span == 0) return KMWS_OK;
+    const WsHead* head = static_cast<const WsHead*>(workspace);
+    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
+    const uint64_t nfull = span / Cfg::kTile;
+    if (nfull > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    if (nfull) {
+        const uint32_t g = (uint32_t)(nfull < grid ? nfull : grid);
+        hipLaunchKernelGGL(unmask_persist_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
+                           (uint32_t)nfull);
+    }
+    if (ntiles > nfull)  // the partial last tile
+        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
+                           (uint32_t)nfull);
+    return hip_status(hipGetLastError());
+}
+
+template <int V>
 static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                  void* workspace, size_t ws_bytes, hipStream_t s)
 {
@@ -355,6 +415,14 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
     case 0: return launch_unmask<4>(base, span, descs, n, workspace, workspace_bytes, s);
     case 1: return launch_unmask<8>(base, span, descs, n, workspace, workspace_bytes, s);
     case 2: return launch_unmask<16>(base, span, descs, n, workspace, workspace_bytes, s);
+    case 3:
+    case 4:
+    case 5: {  // 16 KiB tiles, persistent grid-stride with next-tile prefetch: 4096 / 6144 / 8192 blocks
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        const uint32_t grid = variant == 3 ? 4096u : (variant == 4 ? 6144u : 8192u);
+        return launch_apply_persist<4>(base, span, descs, n, workspace, workspace_bytes, s, grid);
+    }
     default: return KMWS_ERR_INVALID_PARAM;
     }
 }

@@ -165,7 +165,15 @@ int main(int argc, char** argv)
         {"persist2 nt V4 x4096", 12}, {"persist2 nt V4 x8192", 13}, {"persist2 nt V4 x2048", 14},
         {"persist2 V4 x8192", 15}, {"persist2 nt V2 x8192", 16}, {"persist2 nt V8 x4096", 17},
         {"loop nt V4 x4096 (no prefetch)", 18}, {"loop nt V4 x8192 (no prefetch)", 19}, {"persist2 nt V4 x6144", 20},
+        {"product variant 3 (persistent x4096)", 23}, {"product variant 4 (persistent x6144)", 24},
+        {"product variant 5 (persistent x8192)", 25}, {"product variant 0 (default, again)", 26},
     };
+    if (argc > 3) {  // "product": only the product variants, interleaved
+        std::vector<Var> keep;
+        for (auto& v : vars)
+            if (v.kind == 9 || v.kind == 11 || v.kind >= 23) keep.push_back(v);
+        vars = keep;
+    }
     std::vector<std::vector<float>> ms(vars.size());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -196,6 +204,10 @@ int main(int argc, char** argv)
             case 18: hipLaunchKernelGGL((xor_loop<4, 256, true>), dim3(4096), dim3(256), 0, 0, (u32x4*)buf, 0x5au, nw / 1024); break;
             case 19: hipLaunchKernelGGL((xor_loop<4, 256, true>), dim3(8192), dim3(256), 0, 0, (u32x4*)buf, 0x5au, nw / 1024); break;
             case 20: hipLaunchKernelGGL((xor_persist2<4, 256, true>), dim3(6144), dim3(256), 0, 0, (u32x4*)buf, 0x5au, nw / 1024); break;
+            case 23: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 3); break;
+            case 24: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 4); break;
+            case 25: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 5); break;
+            case 26: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 0); break;
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
