@@ -417,10 +417,13 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
     case 2: return launch_unmask<16>(base, span, descs, n, workspace, workspace_bytes, s);
     case 3:
     case 4:
-    case 5: {  // 16 KiB tiles, persistent grid-stride with next-tile prefetch: 4096 / 6144 / 8192 blocks
+    case 5:
+    case 6:
+    case 7: {  // 16 KiB tiles, persistent grid-stride with next-tile prefetch: 4096 .. 16384 blocks
         kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
         if (st != KMWS_OK) return st;
-        const uint32_t grid = variant == 3 ? 4096u : (variant == 4 ? 6144u : 8192u);
+        static const uint32_t grids[] = {8192u, 16384u, 24576u, 32768u, 65536u};
+        const uint32_t grid = grids[variant - 3];
         return launch_apply_persist<4>(base, span, descs, n, workspace, workspace_bytes, s, grid);
     }
     default: return KMWS_ERR_INVALID_PARAM;

@@ -165,8 +165,9 @@ int main(int argc, char** argv)
         {"persist2 nt V4 x4096", 12}, {"persist2 nt V4 x8192", 13}, {"persist2 nt V4 x2048", 14},
         {"persist2 V4 x8192", 15}, {"persist2 nt V2 x8192", 16}, {"persist2 nt V8 x4096", 17},
         {"loop nt V4 x4096 (no prefetch)", 18}, {"loop nt V4 x8192 (no prefetch)", 19}, {"persist2 nt V4 x6144", 20},
-        {"product variant 3 (persistent x4096)", 23}, {"product variant 4 (persistent x6144)", 24},
-        {"product variant 5 (persistent x8192)", 25}, {"product variant 0 (default, again)", 26},
+        {"product variant 3 (persistent x8192)", 23}, {"product variant 4 (persistent x16384)", 24},
+        {"product variant 5 (persistent x24576)", 25}, {"product variant 0 (default, again)", 26},
+        {"product variant 6 (persistent x32768)", 27}, {"product variant 7 (persistent x65536)", 28},
     };
     if (argc > 3) {  // "product": only the product variants, interleaved
         std::vector<Var> keep;
@@ -208,6 +209,8 @@ int main(int argc, char** argv)
             case 24: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 4); break;
             case 25: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 5); break;
             case 26: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 0); break;
+            case 27: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 6); break;
+            case 28: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 7); break;
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
