@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-autotune", action="store_true", help="skip kmws_unmask_autotune (keep the default schedule)")
     return p.parse_args()
 
 
@@ -82,7 +83,7 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def traffic_from_profile(frames: int, frame_len: int):
+def traffic_from_profile(frames: int, frame_len: int, kernel: str):
     """HBM bytes per launch of the unmask kernel from the committed PMC pass
     (profiles/*_traffic.json, written by tools/pmc_traffic.py), if it was
     measured on this exact configuration; else None."""
@@ -93,7 +94,7 @@ def traffic_from_profile(frames: int, frame_len: int):
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if t.get("frames") == frames and t.get("frame_len") == frame_len:
+        if t.get("frames") == frames and t.get("frame_len") == frame_len and t.get("kernel") == kernel:
             best = t
     return None if best is None else best.get("hbm_bytes_per_launch")
 
@@ -150,6 +151,10 @@ def main():
             if ev1 is not None:
                 ev1.record(stream)
 
+    schedule = 0
+    if variant is None and not a.no_autotune:
+        # untimed, payload unchanged: picks this box's faster unmask schedule
+        schedule = kmws.unmask_autotune(base, descs, ws, span)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -187,7 +192,7 @@ def main():
     value = shard.aggregate_rate([span * a.steps] * world, [elapsed] * world) / 2**30
     alg_bytes = n * (2 * L + DESC_BYTES)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profile(n, L)
+    traffic = traffic_from_profile(n, L, "unmask_tiles_kernel" if schedule == 0 else "unmask_persist_kernel")
 
     out = None
     if rank == 0:
@@ -205,11 +210,14 @@ def main():
                        "frames_per_gpu": n, "frame_len": L, "total_frames": n * world,
                        "layout": "aligned arena, frame i at i*frame_len",
                        "parallelism": f"frame-partition x{world} (no collective)",
-                       "tile_variant": "default" if variant is None else variant},
+                       "tile_variant": "default" if variant is None else variant,
+                       "unmask_schedule": "one block per 16 KiB tile" if schedule == 0 else
+                                          f"persistent grid-stride, {schedule} blocks (autotuned)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "unmask_tiles_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "unmask_tiles_kernel" if schedule == 0 else "unmask_persist_kernel",
+                         "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /
                                          (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),

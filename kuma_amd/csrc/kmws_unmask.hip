@@ -145,9 +145,10 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
     }
 }
 
-// One block per tile.
-template <int V>
-__global__ void __launch_bounds__(kBlock) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
+// One block per tile.  W = minimum waves per SIMD the register allocation must
+// allow (1 = unconstrained; the tuning variants test 6 and 8).
+template <int V, int W = 1>
+__global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t tile_base)
@@ -276,6 +277,13 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
 
 // Tile geometry used by the product path (tuned on MI355X).
 constexpr int kUnmaskV = 4;
+
+// Apply schedule per device: 0 = one block per 16 KiB tile (default: 74.5-75 %
+// of HBM peak on every box measured), or a persistent grid-stride grid of that
+// many blocks (+1.5-3 % on most boxes, -12 % on some; profiles/r01_unmask_
+// variants_5boxes.txt).  Set only by kmws_unmask_autotune.
+constexpr int kMaxDevices = 64;
+static uint32_t g_schedule[kMaxDevices];
 using ProdCfg = UnmaskCfg<kUnmaskV>;
 
 static uint32_t ilog2_u64(uint64_t x)
@@ -311,7 +319,7 @@ static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n
     return hip_status(hipGetLastError());
 }
 
-template <int V>
+template <int V, int W = 1>
 static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                 const void* workspace, size_t ws_bytes, hipStream_t s)
 {
@@ -324,8 +332,8 @@ static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* d
     constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
     for (uint64_t t0 = 0; t0 < ntiles; t0 += kMaxBlocks) {
         const uint64_t nb = ntiles - t0 < kMaxBlocks ? ntiles - t0 : kMaxBlocks;
-        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs, n,
-                           reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
+        hipLaunchKernelGGL((unmask_tiles_kernel<V, W>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs,
+                           n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
     }
     return hip_status(hipGetLastError());
 }
@@ -363,6 +371,13 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
 }
 
+static uint32_t current_schedule()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+    return __atomic_load_n(&g_schedule[dev], __ATOMIC_RELAXED);
+}
+
 static bool bad_args(const uint8_t* base, const kmws_desc* descs, uint32_t n, const void* ws)
 {
     return !ws || (n && (!base || !descs)) || (reinterpret_cast<uintptr_t>(base) & 15u);
@@ -385,8 +400,9 @@ kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* des
                               void* workspace, size_t workspace_bytes, void* stream)
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    return launch_unmask<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes,
-                                   static_cast<hipStream_t>(stream));
+    kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+    if (st != KMWS_OK) return st;
+    return kmws_unmask_apply(base, span, descs, n, workspace, workspace_bytes, stream);
 }
 
 kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
@@ -400,8 +416,59 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
                               const void* workspace, size_t workspace_bytes, void* stream)
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    return launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes,
-                                  static_cast<hipStream_t>(stream));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t grid = current_schedule();
+    if (grid) return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s, grid);
+    return launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s);
+}
+
+int kmws_unmask_schedule(void) { return (int)current_schedule(); }
+
+// Times each schedule on the caller's batch, twice per schedule (XOR applied
+// twice is the identity, so the payload is unchanged on return), and keeps the
+// fastest as this device's kmws_unmask_apply schedule.  Synchronizes.
+int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
+                         size_t workspace_bytes, void* stream)
+{
+    if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return KMWS_ERR_FAILED;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
+    if (st != KMWS_OK) return st;
+    static const uint32_t cand[] = {0u, 16384u, 32768u};
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return KMWS_ERR_FAILED;
+    }
+    float best = 1e30f;
+    uint32_t pick = 0;
+    for (int rep = 0; rep < 2; ++rep) {
+        for (uint32_t g : cand) {
+            if (hipEventRecord(e0, s) != hipSuccess) { st = KMWS_ERR_FAILED; break; }
+            for (int k = 0; k < 2 && st == KMWS_OK; ++k)
+                st = g ? launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s, g)
+                       : launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s);
+            if (st != KMWS_OK || hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
+                st = st != KMWS_OK ? st : KMWS_ERR_FAILED;
+                break;
+            }
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (rep == 1 && ms < best) {  // rep 0 warms every schedule up
+                best = ms;
+                pick = g;
+            }
+        }
+        if (st != KMWS_OK) break;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (st != KMWS_OK) return st;
+    __atomic_store_n(&g_schedule[dev], pick, __ATOMIC_RELAXED);
+    return (int)pick;
 }
 
 // Tuning entry: same contract as kmws_unmask_batch with an explicit tile
@@ -425,6 +492,13 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         static const uint32_t grids[] = {8192u, 16384u, 24576u, 32768u, 65536u};
         const uint32_t grid = grids[variant - 3];
         return launch_apply_persist<4>(base, span, descs, n, workspace, workspace_bytes, s, grid);
+    }
+    case 8:
+    case 9: {  // 16 KiB tiles, registers capped for 6 (8) or 8 (9) waves per SIMD
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return variant == 8 ? launch_apply<4, 6>(base, span, descs, n, workspace, workspace_bytes, s)
+                            : launch_apply<4, 8>(base, span, descs, n, workspace, workspace_bytes, s);
     }
     default: return KMWS_ERR_INVALID_PARAM;
     }

@@ -93,7 +93,7 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("variant", [None, 0, 1, 2])
+@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9])
 def test_unmask_parity(torch_dev, kind, variant):
     rng = np.random.default_rng(abs(hash((kind, variant))) % 2**32)
     buf, descs = layout(kind, rng)
@@ -183,4 +183,23 @@ def test_unmask_on_side_stream(torch_dev):
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         got, st = run_gpu(torch, buf, descs, stream=s)
+    assert st == 0 and np.array_equal(got, want)
+
+
+def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
+    """kmws_unmask_autotune runs every schedule twice (XOR twice = identity):
+    the payload is unchanged, and unmask parity holds under the chosen schedule."""
+    torch = torch_dev
+    from kuma_amd import kmws
+    rng = np.random.default_rng(31)
+    buf, descs = layout("packed_wire", rng)
+    d_buf = torch.from_numpy(np.concatenate([buf, np.zeros((-len(buf)) % 16, np.uint8)])).cuda()
+    d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
+    ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
+    choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
+    assert choice in (0, 16384, 32768) and kmws.unmask_schedule() == choice
+    assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
+    want = buf.copy()
+    orc.unmask_batch(want, descs)
+    got, st = run_gpu(torch, buf, descs)
     assert st == 0 and np.array_equal(got, want)

@@ -1,13 +1,20 @@
 #!/bin/bash
-# PMC passes for the headline kernel: FETCH_SIZE and WRITE_SIZE in separate runs
-# (--kernel-trace only beside --pmc), then bytes per launch -> profiles/<tag>_traffic.json
+# PMC passes for the headline kernels: FETCH_SIZE and WRITE_SIZE in separate runs
+# (--kernel-trace only beside --pmc), for the one-block-per-tile schedule and for
+# the persistent schedule (bench --variant 4), -> bytes per launch per kernel.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${RUN_TAG:-r01}
 OUT=gpurun_out/$TAG/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-verify"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/fetch" -o run -- python3 $B > "$OUT/fetch.json" 2> "$OUT/fetch.err" &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/write" -o run -- python3 $B > "$OUT/write.json" 2> "$OUT/write.err" &&
-python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json"
+pass() {  # name counter bench-args
+  timeout -k 10 300 rocprofv3 --pmc "$2" --kernel-trace --output-format csv -d "$PWD/$OUT/$1" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-verify $3 > "$OUT/$1.json" 2> "$OUT/$1.err"
+}
+pass tiles_fetch FETCH_SIZE "--no-autotune" &&
+pass tiles_write WRITE_SIZE "--no-autotune" &&
+python3 tools/pmc_traffic.py "$OUT/tiles_fetch" "$OUT/tiles_write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json" &&
+pass persist_fetch FETCH_SIZE "--variant 4" &&
+pass persist_write WRITE_SIZE "--variant 4" &&
+python3 tools/pmc_traffic.py "$OUT/persist_fetch" "$OUT/persist_write" unmask_persist_kernel 1048576 65536 "$OUT/traffic_persist.json"

@@ -168,6 +168,7 @@ int main(int argc, char** argv)
         {"product variant 3 (persistent x8192)", 23}, {"product variant 4 (persistent x16384)", 24},
         {"product variant 5 (persistent x24576)", 25}, {"product variant 0 (default, again)", 26},
         {"product variant 6 (persistent x32768)", 27}, {"product variant 7 (persistent x65536)", 28},
+        {"product variant 8 (>=6 waves/SIMD)", 29}, {"product variant 9 (>=8 waves/SIMD)", 30},
     };
     if (argc > 3) {  // "product": only the product variants, interleaved
         std::vector<Var> keep;
@@ -211,6 +212,8 @@ int main(int argc, char** argv)
             case 26: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 0); break;
             case 27: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 6); break;
             case 28: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 7); break;
+            case 29: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 8); break;
+            case 30: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 9); break;
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
