@@ -194,13 +194,13 @@ __global__ void __launch_bounds__(kBlock) dst_map_kernel(const uint64_t* __restr
 //   header bytes first (s_hl[j] = 0 for a payload-only gather), then payload
 //   bytes read from src + s_src[j] XOR key byte.
 struct CopyLds {
-    uint64_t dst[kCopyCap];
-    uint64_t src[kCopyCap];
+    uint64_t end[kCopyCap];  // region end (payload end) in the output: the search key
+    uint64_t dst[kCopyCap];  // region start (header start)
+    uint64_t p0[kCopyCap];   // payload start in the output
+    uint64_t sdel[kCopyCap]; // src offset - p0: source byte of output byte a is a + sdel
     uint64_t h0[kCopyCap];
     uint64_t h1[kCopyCap];
-    uint32_t len[kCopyCap];
     uint32_t key[kCopyCap];
-    uint32_t hl[kCopyCap];
 };
 
 // Dword I of the 8-dword window lo||hi (I fixed at compile time).
@@ -259,9 +259,8 @@ __device__ __forceinline__ void load_frame(CopyLds& L, int row, uint32_t fi, con
                                            const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags)
 {
     const kmws_desc x = d[fi];
-    L.dst[row] = start[fi];
-    L.src[row] = x.off;
-    L.len[row] = x.len;
+    const uint64_t r0 = start[fi];
+    uint32_t hl = 0;
     if (HEADERS) {
         const uint32_t fl = flags[fi];
         const uint32_t mask = (fl >> 8) & 1u;
@@ -269,13 +268,16 @@ __device__ __forceinline__ void load_frame(CopyLds& L, int row, uint32_t fi, con
         build_header(x.len, fl, x.key, h0, h1);
         L.h0[row] = h0;
         L.h1[row] = h1;
-        L.hl[row] = hdr_len(x.len, mask);
+        hl = hdr_len(x.len, mask);
         L.key[row] = mask ? x.key : 0u;
     } else {
         L.h0[row] = L.h1[row] = 0;
-        L.hl[row] = 0;
         L.key[row] = x.key;
     }
+    L.dst[row] = r0;
+    L.p0[row] = r0 + hl;
+    L.end[row] = r0 + hl + x.len;
+    L.sdel[row] = x.off - (r0 + hl);  // wraps modulo 2^64; a + sdel is exact
 }
 
 template <bool HEADERS>
@@ -359,31 +361,31 @@ __global__ void __launch_bounds__(kBlock) mask_copy_kernel(const uint8_t* __rest
             int lo = 0, hi = cnt;
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (L.dst[mid] + L.hl[mid] + L.len[mid] <= a) lo = mid + 1; else hi = mid;
+                if (L.end[mid] <= a) lo = mid + 1; else hi = mid;
             }
             for (int j = lo; j < cnt; ++j) {
                 const uint64_t r0 = L.dst[j];
                 if (r0 >= a + 16) break;
-                const uint32_t hlj = L.hl[j], lenj = L.len[j];
-                const uint64_t p0 = r0 + hlj, r1 = p0 + lenj;
+                const uint64_t p0 = L.p0[j], r1 = L.end[j];
                 // header bytes [r0, p0) of frame j that fall in this word
                 if (HEADERS && p0 > a) {
                     const int s = (int)((int64_t)r0 - (int64_t)a);
                     const uint64_t h0 = L.h0[j], h1 = L.h1[j];
                     const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                    out[i] |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, s + (int)hlj > 16 ? 16 : s + (int)hlj);
+                    const int he = (int)(p0 - r0) + s;
+                    out[i] |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
                 }
                 // payload bytes [max(a, p0), min(a + 16, r1)) of frame j
-                if (lenj && p0 < a + 16 && r1 > a) {
+                if (r1 > p0 && p0 < a + 16 && r1 > a) {
                     const uint64_t lo_b = p0 > a ? p0 : a, hi_b = r1 < a + 16 ? r1 : a + 16;
-                    const uint64_t sj = L.src[j];
-                    const uint64_t slo = sj + (lo_b - p0), shi = sj + (hi_b - p0);
+                    const uint64_t sdel = L.sdel[j];
+                    const uint64_t slo = lo_b + sdel, shi = hi_b + sdel;
                     const uint64_t w0 = slo & ~(uint64_t)15, w1 = (shi - 1) & ~(uint64_t)15;
                     const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + w0);
                     const u32x4 W1 = w1 != w0 ? *reinterpret_cast<const u32x4*>(src + w1) : W0;
-                    const int d = (int)((int64_t)(sj + a - p0) - (int64_t)w0);  // in [-15, 15]
-                    const u32x4 V = d >= 0 ? funnel16(W0, W1, (uint32_t)d)
-                                           : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + d));
+                    const int dd = (int)((int64_t)(a + sdel) - (int64_t)w0);  // in [-15, 15]
+                    const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd)
+                                            : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
                     out[i] |= (V ^ rot_key(L.key[j], p0)) & byte_range((int)(lo_b - a), (int)(hi_b - a));
                 }
             }
