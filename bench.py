@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-autotune", action="store_true", help="skip kmws_unmask_autotune (keep the default schedule)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="harness collectives (barrier, max time); nccl = RCCL. gloo lets several ranks share one "
+                        "GPU to rehearse the N>1 path")
     return p.parse_args()
 
 
@@ -108,11 +111,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench: no GPU visible; the HIP path has no CPU fallback")
+    dev = torch.device("cuda", local % ndev)  # one GPU per rank; modulo only when rehearsing on fewer GPUs
     torch.cuda.set_device(dev)
+    if world > 1:
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = dev if a.dist_backend == "nccl" else torch.device("cpu")
     if kmws.device_count() < 1:
         raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
 
@@ -171,7 +180,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
@@ -183,7 +192,7 @@ def main():
             kmws.unmask_batch(base, descs, ws, span)
         mismatches = kmws.check_unmasked(base, seed, descs)
         if world > 1:
-            t = torch.tensor([mismatches], dtype=torch.int64, device=dev)
+            t = torch.tensor([mismatches], dtype=torch.int64, device=coll_dev)
             dist.all_reduce(t)
             mismatches = int(t[0])
 
