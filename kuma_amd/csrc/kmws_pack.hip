@@ -24,9 +24,6 @@ namespace kmws {
 
 constexpr int kScanItems = 8;                      // frames per lane in the scan
 constexpr int kScanTile = kBlock * kScanItems;     // 2048 frames per block
-constexpr int kCopyV = 4;                          // 16-byte words per lane
-constexpr uint64_t kCopyTile = (uint64_t)kBlock * kCopyV * 16;  // 16 KiB of output per block
-constexpr int kCopyCap = kBlock;                   // frames staged per LDS round
 
 __host__ __device__ __forceinline__ uint32_t hdr_len(uint32_t len, uint32_t mask)
 {
@@ -169,40 +166,6 @@ __global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n
     }
 }
 
-// ------------------------------ tile map over the output space ------------------------------
-// Frame f's region in the output is [start[f], start[f+1]); tiles whose first
-// byte falls in it get map = f.  start[n] is the total.
-__global__ void __launch_bounds__(kBlock) dst_map_kernel(const uint64_t* __restrict__ start, uint32_t n,
-                                                         uint64_t cap, uint32_t* __restrict__ map,
-                                                         WsHead* __restrict__ head)
-{
-    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    if (f >= n) return;
-    const uint64_t total = start[n];
-    if (total > cap) {
-        if (f == 0) atomicOr(&head->status, kStatusBadDesc);
-        return;
-    }
-    const uint64_t lo = f == 0 ? 0 : start[f];
-    const uint64_t hi = start[f + 1];
-    for (uint64_t b = (lo + kCopyTile - 1) / kCopyTile; b < (hi + kCopyTile - 1) / kCopyTile; ++b) map[b] = (uint32_t)f;
-}
-
-// ------------------------------ mask-copy emit ------------------------------
-// Output word w (16 bytes at dst + a) for frames staged in LDS:
-//   region j: [s_dst[j], s_dst[j] + s_hl[j] + s_len[j]) of the output,
-//   header bytes first (s_hl[j] = 0 for a payload-only gather), then payload
-//   bytes read from src + s_src[j] XOR key byte.
-struct CopyLds {
-    uint64_t end[kCopyCap];  // region end (payload end) in the output: the search key
-    uint64_t dst[kCopyCap];  // region start (header start)
-    uint64_t p0[kCopyCap];   // payload start in the output
-    uint64_t sdel[kCopyCap]; // src offset - p0: source byte of output byte a is a + sdel
-    uint64_t h0[kCopyCap];
-    uint64_t h1[kCopyCap];
-    uint32_t key[kCopyCap];
-};
-
 // Dword I of the 8-dword window lo||hi (I fixed at compile time).
 template <int I>
 __device__ __forceinline__ uint32_t dw(const u32x4& lo, const u32x4& hi)
@@ -253,158 +216,184 @@ __device__ __forceinline__ u32x4 byte_range(int lo, int hi)
                  dword_byte_mask(lo, hi, 3)};
 }
 
-// Fill a CopyLds row for frame fi; returns the region end.
+// ------------------------------ frame-major mask-copy ------------------------------
+// Output space [0, total) = regions back to back; region f = header (hl bytes,
+// 0 for a payload-only gather) then payload (len bytes) read from
+// src + descs[f].off and XORed with the rotated key.  Output words (16 B,
+// aligned) split into
+//   interior words: fully inside one payload -> interior_kernel, one wave per
+//     unit of 256 words (4 KiB), the source shift uniform per frame, so each
+//     lane loads one aligned word and takes the next from its neighbour;
+//   boundary words: the rest (a word whose first byte lies in a header, or
+//     the word straddling a payload end) -> boundary_kernel, owned by the one
+//     frame whose region holds the word's first byte, composed byte-exactly.
+// Every output byte in [0, total) is written exactly once.
+constexpr int kUnitWords = 256;  // interior words per wave unit (4 words per lane)
+
+struct FrameGeom {
+    uint64_t r0, p0, r1;  // region start, payload start, region end (= payload end)
+    uint64_t sdel;        // source offset - p0 (mod 2^64): source byte of output byte a = a + sdel
+    uint32_t key;         // key to apply (0 = none)
+    uint32_t len;
+};
+
 template <bool HEADERS>
-__device__ __forceinline__ void load_frame(CopyLds& L, int row, uint32_t fi, const uint64_t* __restrict__ start,
-                                           const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags)
+__device__ __forceinline__ FrameGeom geom(uint32_t f, const uint64_t* __restrict__ start,
+                                          const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags)
 {
-    const kmws_desc x = d[fi];
-    const uint64_t r0 = start[fi];
+    const kmws_desc x = d[f];
+    FrameGeom g;
+    g.r0 = start[f];
     uint32_t hl = 0;
+    g.key = x.key;
     if (HEADERS) {
-        const uint32_t fl = flags[fi];
-        const uint32_t mask = (fl >> 8) & 1u;
-        uint64_t h0, h1;
-        build_header(x.len, fl, x.key, h0, h1);
-        L.h0[row] = h0;
-        L.h1[row] = h1;
+        const uint32_t mask = (flags[f] >> 8) & 1u;
         hl = hdr_len(x.len, mask);
-        L.key[row] = mask ? x.key : 0u;
-    } else {
-        L.h0[row] = L.h1[row] = 0;
-        L.key[row] = x.key;
+        if (!mask) g.key = 0;
     }
-    L.dst[row] = r0;
-    L.p0[row] = r0 + hl;
-    L.end[row] = r0 + hl + x.len;
-    L.sdel[row] = x.off - (r0 + hl);  // wraps modulo 2^64; a + sdel is exact
+    g.p0 = g.r0 + hl;
+    g.r1 = g.p0 + x.len;
+    g.sdel = x.off - g.p0;
+    g.len = x.len;
+    return g;
+}
+
+// Interior word range [wlo, whi) of a frame and its number of wave units.
+__device__ __forceinline__ void interior(const FrameGeom& g, uint64_t& wlo, uint64_t& whi)
+{
+    wlo = (g.p0 + 15) >> 4;
+    whi = g.r1 >> 4;
+    if (whi < wlo) whi = wlo;
 }
 
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) mask_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                           const uint64_t* __restrict__ start,
-                                                           const kmws_desc* __restrict__ d,
-                                                           const uint16_t* __restrict__ flags, uint32_t n,
-                                                           const uint32_t* __restrict__ map,
-                                                           const WsHead* __restrict__ head, uint32_t tile_base)
-{
-    __shared__ CopyLds L;
-    const uint32_t tile = tile_base + blockIdx.x;
-    const uint64_t total = start[n];
-    const uint64_t tile_lo = (uint64_t)tile * kCopyTile;
-    if (tile_lo >= total || head->status != 0) return;  // uniform
-    const uint64_t tile_hi = tile_lo + kCopyTile < total ? tile_lo + kCopyTile : total;
-    const int tid = threadIdx.x;
-    uint32_t f = map[tile];
-
-    // Fast path: the whole tile is payload of one frame (uniform scalars).
+struct UnitCount {
+    const uint64_t* start;
+    const kmws_desc* d;
+    const uint16_t* flags;
+    __device__ uint64_t operator()(uint32_t f) const
     {
-        const uint64_t r0 = start[f];
-        const kmws_desc x = d[f];
-        const uint32_t hl = HEADERS ? hdr_len(x.len, (flags[f] >> 8) & 1u) : 0u;
-        const uint64_t p0 = r0 + hl;
-        const bool masked = HEADERS ? ((flags[f] >> 8) & 1u) != 0 : true;
-        if (tile_lo + kCopyTile <= total && p0 <= tile_lo && p0 + x.len >= tile_lo + kCopyTile) {
-            const uint32_t rk = masked ? rot_key(x.key, p0) : 0u;
-            // source byte of output byte a: x.off + (a - p0); shift = its misalignment
-            const uint64_t sbase = x.off + (tile_lo - p0);
-            const uint32_t delta = (uint32_t)(sbase & 15u);
-            const uint8_t* s0 = src + (sbase - delta);
-            u32x4 lo[kCopyV], hi[kCopyV];
-#pragma unroll
-            for (int i = 0; i < kCopyV; ++i) {
-                const uint64_t w = (uint64_t)(tid + kBlock * i);
-                lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16 * w));
-            }
-            if (delta != 0) {
-                // the next aligned word: from lane+1 by a cross-lane move, lane 63 loads it
-                const int lane = tid & 63;
-#pragma unroll
-                for (int i = 0; i < kCopyV; ++i) {
-                    const uint64_t w = (uint64_t)(tid + kBlock * i);
-                    u32x4 nx;
-                    nx.x = __shfl_down(lo[i].x, 1, 64);
-                    nx.y = __shfl_down(lo[i].y, 1, 64);
-                    nx.z = __shfl_down(lo[i].z, 1, 64);
-                    nx.w = __shfl_down(lo[i].w, 1, 64);
-                    if (lane == 63) nx = *reinterpret_cast<const u32x4*>(s0 + 16 * (w + 1));
-                    hi[i] = nx;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < kCopyV; ++i) {
-                const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-                const u32x4 v = delta ? funnel16(lo[i], hi[i], delta) : lo[i];
-                __builtin_nontemporal_store(v ^ rk, reinterpret_cast<u32x4*>(dst + a));
-            }
-            return;
-        }
+        const FrameGeom g = geom<HEADERS>(f, start, d, flags);
+        uint64_t wlo, whi;
+        interior(g, wlo, whi);
+        return (whi - wlo + kUnitWords - 1) / kUnitWords;
     }
+};
 
-    // General path: stage every frame overlapping the tile, compose bytes.
-    u32x4 out[kCopyV];
+// unit -> frame map; also the capacity check (status set if total > cap).
+__global__ void __launch_bounds__(kBlock) unit_map_kernel(const uint64_t* __restrict__ start,
+                                                          const uint64_t* __restrict__ unit_off, uint32_t n,
+                                                          uint64_t cap, uint32_t* __restrict__ umap,
+                                                          WsHead* __restrict__ head)
+{
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n) return;
+    if (start[n] > cap) {
+        if (f == 0) atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    for (uint64_t u = unit_off[f]; u < unit_off[f + 1]; ++u) umap[u] = f;
+}
+
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          const uint64_t* __restrict__ start,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          const uint64_t* __restrict__ unit_off,
+                                                          const uint32_t* __restrict__ umap,
+                                                          const WsHead* __restrict__ head, uint64_t unit_base)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t u = unit_base + (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (u >= unit_off[n] || head->status != 0) return;  // wave-uniform
+    const uint32_t f = umap[u];
+    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
+    uint64_t wlo, whi;
+    interior(g, wlo, whi);
+    const uint64_t w0 = wlo + (u - unit_off[f]) * kUnitWords;
+    const uint32_t rk = g.key ? rot_key(g.key, g.p0) : 0u;
+    const uint32_t delta = (uint32_t)((16u * wlo + g.sdel) & 15u);  // same for every word of the frame
+    u32x4 lo[kUnitWords / 64];
 #pragma unroll
-    for (int i = 0; i < kCopyV; ++i) out[i] = u32x4{0, 0, 0, 0};
-    for (;;) {
-        const uint32_t fi = f + (uint32_t)tid;
-        int valid = 0;
-        if (fi < n && start[fi] < tile_hi) {
-            load_frame<HEADERS>(L, tid, fi, start, d, flags);
-            valid = 1;
+    for (int i = 0; i < kUnitWords / 64; ++i) {
+        const uint64_t w = w0 + lane + 64 * i;
+        const uint64_t sb = 16u * w + g.sdel - delta;
+        lo[i] = w < whi ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + sb)) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < kUnitWords / 64; ++i) {
+        const uint64_t w = w0 + lane + 64 * i;
+        u32x4 v = lo[i];
+        if (delta) {
+            u32x4 hi;
+            hi.x = __shfl_down(lo[i].x, 1, 64);
+            hi.y = __shfl_down(lo[i].y, 1, 64);
+            hi.z = __shfl_down(lo[i].z, 1, 64);
+            hi.w = __shfl_down(lo[i].w, 1, 64);
+            // the neighbour's word is not this lane's next source word: load it
+            if ((lane == 63 || w + 1 >= whi) && w < whi)
+                hi = *reinterpret_cast<const u32x4*>(src + 16u * w + g.sdel - delta + 16);
+            v = funnel16(lo[i], hi, delta);
         }
-        const int cnt = __syncthreads_count(valid);
-#pragma unroll
-        for (int i = 0; i < kCopyV; ++i) {
-            const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-            if (a >= tile_hi) continue;
-            // first staged frame whose region ends after a
-            int lo = 0, hi = cnt;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (L.end[mid] <= a) lo = mid + 1; else hi = mid;
-            }
-            for (int j = lo; j < cnt; ++j) {
-                const uint64_t r0 = L.dst[j];
-                if (r0 >= a + 16) break;
-                const uint64_t p0 = L.p0[j], r1 = L.end[j];
-                // header bytes [r0, p0) of frame j that fall in this word
-                if (HEADERS && p0 > a) {
-                    const int s = (int)((int64_t)r0 - (int64_t)a);
-                    const uint64_t h0 = L.h0[j], h1 = L.h1[j];
+        if (w < whi) __builtin_nontemporal_store(v ^ rk, reinterpret_cast<u32x4*>(dst + 16u * w));
+    }
+}
+
+// One lane per frame: the boundary words whose first byte lies in this frame's
+// region: [ceil(r0/16), ceil(p0/16)) (header words) and the word straddling the
+// payload end, composed from every frame that overlaps them.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) boundary_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          const uint64_t* __restrict__ start,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          const WsHead* __restrict__ head)
+{
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n || head->status != 0) return;
+    const uint64_t total = start[n];
+    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
+    const uint64_t a_hdr0 = (g.r0 + 15) >> 4, a_hdr1 = (g.p0 + 15) >> 4;
+    const uint64_t b0 = (g.r1 >> 4) > a_hdr1 ? (g.r1 >> 4) : a_hdr1, b1 = (g.r1 + 15) >> 4;
+    for (int part = 0; part < 2; ++part) {
+        const uint64_t wa = part == 0 ? a_hdr0 : b0, wb = part == 0 ? a_hdr1 : b1;
+        for (uint64_t w = wa; w < wb; ++w) {
+            const uint64_t a = 16u * w;
+            u32x4 out = u32x4{0, 0, 0, 0};
+            for (uint32_t j = f; j < n; ++j) {
+                const FrameGeom h = j == f ? g : geom<HEADERS>(j, start, d, flags);
+                if (h.r0 >= a + 16) break;
+                if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
+                    const kmws_desc x = d[j];
+                    uint64_t h0, h1;
+                    build_header(x.len, flags[j], x.key, h0, h1);
+                    const int s = (int)((int64_t)h.r0 - (int64_t)a);
                     const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                    const int he = (int)(p0 - r0) + s;
-                    out[i] |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
+                    const int he = (int)(h.p0 - h.r0) + s;
+                    out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
                 }
-                // payload bytes [max(a, p0), min(a + 16, r1)) of frame j
-                if (r1 > p0 && p0 < a + 16 && r1 > a) {
-                    const uint64_t lo_b = p0 > a ? p0 : a, hi_b = r1 < a + 16 ? r1 : a + 16;
-                    const uint64_t sdel = L.sdel[j];
-                    const uint64_t slo = lo_b + sdel, shi = hi_b + sdel;
-                    const uint64_t w0 = slo & ~(uint64_t)15, w1 = (shi - 1) & ~(uint64_t)15;
-                    const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + w0);
-                    const u32x4 W1 = w1 != w0 ? *reinterpret_cast<const u32x4*>(src + w1) : W0;
-                    const int dd = (int)((int64_t)(a + sdel) - (int64_t)w0);  // in [-15, 15]
+                if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
+                    const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+                    const uint64_t slo = lo_b + h.sdel, shi = hi_b + h.sdel;
+                    const uint64_t s0 = slo & ~(uint64_t)15, s1 = (shi - 1) & ~(uint64_t)15;
+                    const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + s0);
+                    const u32x4 W1 = s1 != s0 ? *reinterpret_cast<const u32x4*>(src + s1) : W0;
+                    const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
                     const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd)
                                             : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
-                    out[i] |= (V ^ rot_key(L.key[j], p0)) & byte_range((int)(lo_b - a), (int)(hi_b - a));
+                    const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
+                    out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
                 }
             }
-        }
-        if (cnt < kCopyCap) break;
-        f += kCopyCap;
-        __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < kCopyV; ++i) {
-        const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-        if (a + 16 <= tile_hi) {
-            __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + a));
-        } else if (a < tile_hi) {  // last partial word of the output: byte stores
-            const u32x4 o = out[i];
-            for (uint64_t p = a; p < tile_hi; ++p) {
-                const uint32_t k = (uint32_t)(p - a);
-                const uint32_t dw = (k & 8u) ? ((k & 4u) ? o.w : o.z) : ((k & 4u) ? o.y : o.x);
-                dst[p] = (uint8_t)(dw >> (8 * (k & 3u)));
+            if (a + 16 <= total) {
+                *reinterpret_cast<u32x4*>(dst + a) = out;
+            } else {  // last partial word of the output: byte stores
+                for (uint64_t p = a; p < total; ++p) {
+                    const uint32_t k = (uint32_t)(p - a);
+                    const uint32_t dwv = (k & 8u) ? ((k & 4u) ? out.w : out.z) : ((k & 4u) ? out.y : out.x);
+                    dst[p] = (uint8_t)(dwv >> (8 * (k & 3u)));
+                }
             }
         }
     }
@@ -494,16 +483,17 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
 struct CopyWs {
     WsHead* head;
     uint64_t* partials;
-    uint32_t* map;
+    uint64_t* unit_off;
+    uint32_t* umap;
 };
 
 static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
+static uint64_t max_units(uint32_t n, uint64_t cap) { return (cap + kUnitWords * 16 - 1) / (kUnitWords * 16) + n; }
+static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    const uint64_t nb = n_scan_blocks(n) + 1;
-    const uint64_t nt = (cap + kCopyTile - 1) / kCopyTile;
-    return sizeof(WsHead) + ((nb * 8 + 15) & ~15ull) + nt * 4;
+    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * 8) + r16(((uint64_t)n + 1) * 8) + max_units(n, cap) * 4;
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -511,9 +501,12 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     if (!ws || ws_bytes < copy_ws_size(n, cap)) return false;
     char* p = static_cast<char*>(ws);
     c.head = reinterpret_cast<WsHead*>(p);
-    c.partials = reinterpret_cast<uint64_t*>(p + sizeof(WsHead));
-    const uint64_t nb = n_scan_blocks(n) + 1;
-    c.map = reinterpret_cast<uint32_t*>(p + sizeof(WsHead) + ((nb * 8 + 15) & ~15ull));
+    p += sizeof(WsHead);
+    c.partials = reinterpret_cast<uint64_t*>(p);
+    p += r16((n_scan_blocks(n) + 1) * 8);
+    c.unit_off = reinterpret_cast<uint64_t*>(p);
+    p += r16(((uint64_t)n + 1) * 8);
+    c.umap = reinterpret_cast<uint32_t*>(p);
     return true;
 }
 
@@ -532,15 +525,19 @@ template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, const uint64_t* start,
                                const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
-    hipLaunchKernelGGL(dst_map_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, start, n, cap, c.map,
-                       c.head);
-    const uint64_t ntiles = (cap + kCopyTile - 1) / kCopyTile;
-    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
-    for (uint64_t t0 = 0; t0 < ntiles; t0 += kMaxBlocks) {
-        const uint64_t nb = ntiles - t0 < kMaxBlocks ? ntiles - t0 : kMaxBlocks;
-        hipLaunchKernelGGL(mask_copy_kernel<HEADERS>, dim3((uint32_t)nb), dim3(kBlock), 0, s, src, dst, start, d,
-                           flags, n, c.map, c.head, (uint32_t)t0);
+    kmws_status st = launch_scan(UnitCount<HEADERS>{start, d, flags}, n, c.unit_off, c.partials, s);
+    if (st != KMWS_OK) return st;
+    const uint32_t fb = (n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(unit_map_kernel, dim3(fb), dim3(kBlock), 0, s, start, c.unit_off, n, cap, c.umap, c.head);
+    const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
+    constexpr uint64_t kWavesPerBlock = kBlock / 64;
+    constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
+    for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
+        const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
+        hipLaunchKernelGGL(interior_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), 0, s, src, dst, start, d, flags, n, c.unit_off, c.umap, c.head, u0);
     }
+    hipLaunchKernelGGL(boundary_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, src, dst, start, d, flags, n, c.head);
     return hip_status(hipGetLastError());
 }
 
