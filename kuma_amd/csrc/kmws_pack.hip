@@ -280,10 +280,24 @@ struct UnitCount {
     }
 };
 
-// unit -> frame map; also the capacity check (status set if total > cap).
-__global__ void __launch_bounds__(kBlock) unit_map_kernel(const uint64_t* __restrict__ start,
+// One record per interior unit, written by the unit's frame: everything a
+// wave needs in one 32-byte scalar load.
+struct UnitRec {
+    uint64_t dst;     // output byte of the unit's first word (16-B aligned)
+    uint64_t src;     // source byte of that word (any alignment)
+    uint32_t nwords;  // 1..kUnitWords
+    uint32_t rk;      // rotated key for the unit's aligned output words (0 = no mask)
+    uint64_t pad;
+};
+static_assert(sizeof(UnitRec) == 32, "UnitRec is one s_load_dwordx8");
+
+// Per-unit records; also the capacity check (status set if total > cap).
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __restrict__ start,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags,
                                                           const uint64_t* __restrict__ unit_off, uint32_t n,
-                                                          uint64_t cap, uint32_t* __restrict__ umap,
+                                                          uint64_t cap, UnitRec* __restrict__ rec,
                                                           WsHead* __restrict__ head)
 {
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
@@ -292,38 +306,52 @@ __global__ void __launch_bounds__(kBlock) unit_map_kernel(const uint64_t* __rest
         if (f == 0) atomicOr(&head->status, kStatusBadDesc);
         return;
     }
-    for (uint64_t u = unit_off[f]; u < unit_off[f + 1]; ++u) umap[u] = f;
-}
-
-template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                          const uint64_t* __restrict__ start,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags, uint32_t n,
-                                                          const uint64_t* __restrict__ unit_off,
-                                                          const uint32_t* __restrict__ umap,
-                                                          const WsHead* __restrict__ head, uint64_t unit_base)
-{
-    const int lane = threadIdx.x & 63;
-    const uint64_t u = unit_base + (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (u >= unit_off[n] || head->status != 0) return;  // wave-uniform
-    const uint32_t f = umap[u];
     const FrameGeom g = geom<HEADERS>(f, start, d, flags);
     uint64_t wlo, whi;
     interior(g, wlo, whi);
-    const uint64_t w0 = wlo + (u - unit_off[f]) * kUnitWords;
     const uint32_t rk = g.key ? rot_key(g.key, g.p0) : 0u;
-    const uint32_t delta = (uint32_t)((16u * wlo + g.sdel) & 15u);  // same for every word of the frame
+    uint64_t w = wlo;
+    for (uint64_t u = unit_off[f]; u < unit_off[f + 1]; ++u, w += kUnitWords) {
+        UnitRec r;
+        r.dst = 16u * w;
+        r.src = 16u * w + g.sdel;
+        r.nwords = (uint32_t)(whi - w < (uint64_t)kUnitWords ? whi - w : (uint64_t)kUnitWords);
+        r.rk = rk;
+        r.pad = 0;
+        rec[u] = r;
+    }
+}
+
+// One wave per interior unit: 4 words per lane, 1 KiB per wave-instruction.
+__global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          const uint64_t* __restrict__ unit_off, uint32_t n,
+                                                          const UnitRec* __restrict__ rec,
+                                                          const WsHead* __restrict__ head, uint64_t unit_base)
+{
+    const int lane = threadIdx.x & 63;
+    // wave id through readfirstlane: provably uniform, so the record is one scalar load
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t u = unit_base + (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    // record, unit count and status are independent scalar loads (one latency
+    // level); records past the count lie inside the workspace and are ignored
+    const UnitRec r = rec[u];
+    const uint64_t total_units = unit_off[n];
+    const uint32_t st = head->status;
+    // no early exit between these loads and their uses (the compiler would sink
+    // the record load below the count's wait): an out-of-range wave has 0 words
+    const uint32_t nwords = (u < total_units && st == 0) ? r.nwords : 0u;
+    const uint32_t delta = (uint32_t)(r.src & 15u);   // same for every word of the unit
+    const uint8_t* s0 = src + (r.src - delta);
     u32x4 lo[kUnitWords / 64];
 #pragma unroll
     for (int i = 0; i < kUnitWords / 64; ++i) {
-        const uint64_t w = w0 + lane + 64 * i;
-        const uint64_t sb = 16u * w + g.sdel - delta;
-        lo[i] = w < whi ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + sb)) : u32x4{0, 0, 0, 0};
+        const uint32_t k = lane + 64 * i;
+        lo[i] = k < nwords ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * k))
+                             : u32x4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int i = 0; i < kUnitWords / 64; ++i) {
-        const uint64_t w = w0 + lane + 64 * i;
+        const uint32_t k = lane + 64 * i;
         u32x4 v = lo[i];
         if (delta) {
             u32x4 hi;
@@ -332,11 +360,11 @@ __global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restr
             hi.z = __shfl_down(lo[i].z, 1, 64);
             hi.w = __shfl_down(lo[i].w, 1, 64);
             // the neighbour's word is not this lane's next source word: load it
-            if ((lane == 63 || w + 1 >= whi) && w < whi)
-                hi = *reinterpret_cast<const u32x4*>(src + 16u * w + g.sdel - delta + 16);
+            if ((lane == 63 || k + 1 >= nwords) && k < nwords)
+                hi = *reinterpret_cast<const u32x4*>(s0 + 16u * k + 16);
             v = funnel16(lo[i], hi, delta);
         }
-        if (w < whi) __builtin_nontemporal_store(v ^ rk, reinterpret_cast<u32x4*>(dst + 16u * w));
+        if (k < nwords) __builtin_nontemporal_store(v ^ r.rk, reinterpret_cast<u32x4*>(dst + r.dst + 16u * k));
     }
 }
 
@@ -484,7 +512,7 @@ struct CopyWs {
     WsHead* head;
     uint64_t* partials;
     uint64_t* unit_off;
-    uint32_t* umap;
+    UnitRec* rec;
 };
 
 static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
@@ -493,7 +521,8 @@ static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * 8) + r16(((uint64_t)n + 1) * 8) + max_units(n, cap) * 4;
+    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * 8) + r16(((uint64_t)n + 1) * 8) +
+           max_units(n, cap) * sizeof(UnitRec);
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -506,7 +535,7 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     p += r16((n_scan_blocks(n) + 1) * 8);
     c.unit_off = reinterpret_cast<uint64_t*>(p);
     p += r16(((uint64_t)n + 1) * 8);
-    c.umap = reinterpret_cast<uint32_t*>(p);
+    c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
 }
 
@@ -528,14 +557,15 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     kmws_status st = launch_scan(UnitCount<HEADERS>{start, d, flags}, n, c.unit_off, c.partials, s);
     if (st != KMWS_OK) return st;
     const uint32_t fb = (n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(unit_map_kernel, dim3(fb), dim3(kBlock), 0, s, start, c.unit_off, n, cap, c.umap, c.head);
+    hipLaunchKernelGGL(unit_rec_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, start, d, flags, c.unit_off, n, cap,
+                       c.rec, c.head);
     const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
     constexpr uint64_t kWavesPerBlock = kBlock / 64;
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
     for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
         const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
-        hipLaunchKernelGGL(interior_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kBlock), 0, s, src, dst, start, d, flags, n, c.unit_off, c.umap, c.head, u0);
+        hipLaunchKernelGGL(interior_kernel, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), 0, s, src, dst, c.unit_off, n, c.rec, c.head, u0);
     }
     hipLaunchKernelGGL(boundary_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, src, dst, start, d, flags, n, c.head);
     return hip_status(hipGetLastError());
