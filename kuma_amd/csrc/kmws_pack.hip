@@ -341,16 +341,32 @@ __global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restr
     // the record load below the count's wait): an out-of-range wave has 0 words
     const uint32_t nwords = (u < total_units && st == 0) ? r.nwords : 0u;
     const uint32_t delta = (uint32_t)(r.src & 15u);   // same for every word of the unit
+    if (nwords == 0) return;                            // wave-uniform, after the record's wait
     const uint8_t* s0 = src + (r.src - delta);
-    u32x4 lo[kUnitWords / 64];
+    const uint32_t last = nwords - 1;
+    constexpr int kW = kUnitWords / 64;
+    // Every load is issued before the first store (vmcnt also counts stores, so
+    // a load issued after a store would make its wait cover that store too).
+    // Addresses are clamped to the unit instead of predicating the loads.
+    u32x4 lo[kW], ex[kW];
 #pragma unroll
-    for (int i = 0; i < kUnitWords / 64; ++i) {
+    for (int i = 0; i < kW; ++i) {
         const uint32_t k = lane + 64 * i;
-        lo[i] = k < nwords ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * k))
-                             : u32x4{0, 0, 0, 0};
+        lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * (k < last ? k : last)));
     }
+    if (delta) {
+        // the next aligned source word comes from lane + 1, except on lane 63
+        // and on the unit's last word, which load it themselves
 #pragma unroll
-    for (int i = 0; i < kUnitWords / 64; ++i) {
+        for (int i = 0; i < kW; ++i) {
+            const uint32_t k = lane + 64 * i;
+            if (lane == 63 || k >= last)
+                ex[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * ((k < last ? k : last) + 1));
+        }
+    }
+    u32x4 out[kW];
+#pragma unroll
+    for (int i = 0; i < kW; ++i) {
         const uint32_t k = lane + 64 * i;
         u32x4 v = lo[i];
         if (delta) {
@@ -359,12 +375,15 @@ __global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restr
             hi.y = __shfl_down(lo[i].y, 1, 64);
             hi.z = __shfl_down(lo[i].z, 1, 64);
             hi.w = __shfl_down(lo[i].w, 1, 64);
-            // the neighbour's word is not this lane's next source word: load it
-            if ((lane == 63 || k + 1 >= nwords) && k < nwords)
-                hi = *reinterpret_cast<const u32x4*>(s0 + 16u * k + 16);
+            if (lane == 63 || k >= last) hi = ex[i];
             v = funnel16(lo[i], hi, delta);
         }
-        if (k < nwords) __builtin_nontemporal_store(v ^ r.rk, reinterpret_cast<u32x4*>(dst + r.dst + 16u * k));
+        out[i] = v ^ r.rk;
+    }
+#pragma unroll
+    for (int i = 0; i < kW; ++i) {
+        const uint32_t k = lane + 64 * i;
+        if (k < nwords) __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + r.dst + 16u * k));
     }
 }
 
