@@ -4,20 +4,21 @@
 // (src/ws/WSHandler.cpp:46-106) followed by the masked payload
 // (WebSocket::Impl::sendWsFrame, src/ws/WebSocketImpl.cpp:381-404): the wire
 // image is header_0 payload_0 header_1 payload_1 ...  Kernels:
-//   1. scan_reduce / scan_partials / scan_emit: exclusive scan of the wire
-//      size (2/4/10 + 4*mask + len) of every frame -> wire_off[0..n]
-//      (wave prefix sums with __shfl_up, one LDS round across the 4 waves);
-//   2. dst_map: tile -> first frame over the output byte space;
-//   3. mask_copy: every 16-byte output word is produced by exactly one lane:
-//      header bytes come from a 14-byte header built in registers, payload
-//      bytes from the source (funnel-shifted when source and destination are
-//      misaligned) XOR the rotated key.  Outputs are written once, with no
-//      read-modify-write.
+//   1. scan_reduce / scan_partials / scan_emit: one exclusive scan of two
+//      per-frame values -- the wire size (2/4/10 + 4*mask + len) -> wire_off,
+//      and an upper bound on the frame's wave units -> unit slot bases;
+//   2. unit_rec: one 32-byte record per wave unit (slots written coalesced);
+//      edge_kernel: the few words around each frame boundary (header bytes,
+//      the next frame's first bytes), composed byte-exactly;
+//   3. copy_kernel: one wave per unit of a frame's owned 64-byte granules;
+//      interior words are loaded, funnel-shifted and XORed with the rotated
+//      key, edge words are merged in; every granule is written once, by one
+//      store instruction.
 // Decode (descriptor-indexed): kmws_unpack_headers parses and
 // validates one header per frame with the reference's rules
 // (WSHandler.cpp:118-234, including the 127-length quirk); the payload is then
 // unmasked in place (kmws_unmask_batch) or gathered + unmasked into a dense
-// arena by the same mask_copy kernel (kmws_gather_unmask).
+// arena by the same copy kernels (kmws_gather_unmask).
 #include "kmws_common.hpp"
 
 namespace kmws {
@@ -68,19 +69,50 @@ __device__ __forceinline__ void build_header(uint32_t len, uint32_t flags, uint3
 }
 
 // ------------------------------ scan ------------------------------
-// size(f) for the two users: encode (header + payload) and gather (payload).
+// One pass scans two per-frame quantities: the region size (header + payload
+// for encode, payload for gather) -> region offsets, and an upper bound on the
+// frame's wave units (it depends on the region size only) -> unit slot bases.
+struct V2 {
+    uint64_t a, b;
+};
+__device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b + y.b}; }
+
+constexpr int kUnitWords = 256;   // output words per wave unit (4 per lane)
+constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
+#ifndef KMWS_LINE_BYTES
+#define KMWS_LINE_BYTES 64
+#endif
+constexpr uint64_t kLineBytes = KMWS_LINE_BYTES;  // ownership granule: 64 B keeps a frame edge at 1 + 4 words
+constexpr uint64_t kLineWords = kLineBytes / 16;
+constexpr int kEdgeWords = 1 + (int)kLineWords;   // owned non-interior words per frame (at most)
+
+// Wave units of a region of R bytes, whatever its offset: a region holds at most
+// ceil(R/kLineBytes) granule starts, and the first unit's base lies at most
+// 64 - kLineWords words below the first owned word.
+__host__ __device__ __forceinline__ uint64_t unit_bound(uint64_t R)
+{
+    if (R == 0) return 0;
+    return (kLineWords * ((R + kLineBytes - 1) / kLineBytes) + (kUnitAlign - kLineWords) + kUnitWords - 1) /
+           kUnitWords;
+}
+
 struct WireSize {
     const kmws_desc* d;
     const uint16_t* flags;
-    __device__ uint64_t operator()(uint32_t f) const
+    __device__ V2 operator()(uint32_t f) const
     {
         const uint32_t len = d[f].len;
-        return (uint64_t)hdr_len(len, (flags[f] >> 8) & 1u) + len;
+        const uint64_t r = (uint64_t)hdr_len(len, (flags[f] >> 8) & 1u) + len;
+        return V2{r, unit_bound(r)};
     }
 };
 struct PayloadSize {
     const kmws_desc* d;
-    __device__ uint64_t operator()(uint32_t f) const { return d[f].len; }
+    __device__ V2 operator()(uint32_t f) const
+    {
+        const uint64_t r = d[f].len;
+        return V2{r, unit_bound(r)};
+    }
 };
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x)
@@ -94,75 +126,103 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x)
     return x;
 }
 
-// Block-wide exclusive scan of one value per lane; returns the block total too.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t x, uint64_t* s_wave, uint64_t& total)
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x)
 {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t inc = wave_incl_scan(x);
-    if (lane == 63) s_wave[wave] = inc;
-    __syncthreads();
-    uint64_t before = 0;
-    total = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
-        const uint64_t v = s_wave[w];
-        if (w < wave) before += v;
-        total += v;
-    }
-    __syncthreads();
-    return before + inc - x;
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
 }
 
+// Frames of a scan block are read row-striped (frame base + i*kBlock + tid), so
+// every load instruction is coalesced.
 template <class Size>
-__global__ void __launch_bounds__(kBlock) scan_reduce_kernel(Size size, uint32_t n, uint64_t* __restrict__ partials)
+__global__ void __launch_bounds__(kBlock) scan_reduce_kernel(Size size, uint32_t n, V2* __restrict__ partials)
 {
-    __shared__ uint64_t s_wave[kBlock / 64];
-    const uint32_t f0 = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    uint64_t s = 0;
+    __shared__ V2 s_wave[kBlock / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
+    V2 s{0, 0};
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i)
-        if (f0 + i < n) s += size(f0 + i);
-    uint64_t total;
-    block_excl_scan(s, s_wave, total);
-    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = base + (uint64_t)i * kBlock;
+        if (f < n) s = s + size((uint32_t)f);
+    }
+    s.a = wave_sum(s.a);
+    s.b = wave_sum(s.b);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        V2 t{0, 0};
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) t = t + s_wave[w];
+        partials[blockIdx.x] = t;
+    }
 }
 
-// One block scans the per-block totals in place (exclusive) and writes the grand total.
-__global__ void __launch_bounds__(kBlock) scan_partials_kernel(uint64_t* __restrict__ partials, uint32_t nb,
-                                                               uint64_t* __restrict__ total_out)
+// One block scans the per-block totals in place (exclusive) and writes the grand totals.
+__global__ void __launch_bounds__(kBlock) scan_partials_kernel(V2* __restrict__ partials, uint32_t nb,
+                                                               uint64_t* __restrict__ total_a,
+                                                               uint64_t* __restrict__ total_b)
 {
-    __shared__ uint64_t s_wave[kBlock / 64];
-    uint64_t carry = 0;
+    __shared__ V2 s_wave[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    V2 carry{0, 0};
     for (uint32_t base = 0; base < nb; base += kBlock) {
         const uint32_t i = base + threadIdx.x;
-        const uint64_t x = i < nb ? partials[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan(x, s_wave, tot);
-        if (i < nb) partials[i] = carry + ex;
-        carry += tot;
+        const V2 x = i < nb ? partials[i] : V2{0, 0};
+        const V2 inc{wave_incl_scan(x.a), wave_incl_scan(x.b)};
+        if (lane == 63) s_wave[wave] = inc;
+        __syncthreads();
+        V2 before{0, 0}, tot{0, 0};
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const V2 v = s_wave[w];
+            if (w < wave) before = before + v;
+            tot = tot + v;
+        }
+        __syncthreads();
+        if (i < nb) partials[i] = V2{carry.a + before.a + inc.a - x.a, carry.b + before.b + inc.b - x.b};
+        carry = carry + tot;
     }
-    if (threadIdx.x == 0) *total_out = carry;
+    if (threadIdx.x == 0) {
+        *total_a = carry.a;
+        *total_b = carry.b;
+    }
 }
 
 template <class Size>
-__global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n, const uint64_t* __restrict__ partials,
-                                                           uint64_t* __restrict__ out)
+__global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n, const V2* __restrict__ partials,
+                                                           uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b)
 {
-    __shared__ uint64_t s_wave[kBlock / 64];
-    const uint32_t f0 = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    uint64_t v[kScanItems];
-    uint64_t s = 0;
+    __shared__ V2 s_row[kScanItems][kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
+    V2 ex[kScanItems];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
-        v[i] = f0 + i < n ? size(f0 + i) : 0;
-        s += v[i];
+        const uint64_t f = base + (uint64_t)i * kBlock;
+        const V2 v = f < n ? size((uint32_t)f) : V2{0, 0};
+        const V2 inc{wave_incl_scan(v.a), wave_incl_scan(v.b)};
+        ex[i] = V2{inc.a - v.a, inc.b - v.b};
+        if (lane == 63) s_row[i][wave] = inc;
     }
-    uint64_t total;
-    uint64_t run = partials[blockIdx.x] + block_excl_scan(s, s_wave, total);
+    __syncthreads();
+    // frame (i, wave, lane) follows rows < i (all waves) and waves < wave of row i
+    V2 run = partials[blockIdx.x];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
-        if (f0 + i < n) out[f0 + i] = run;
-        run += v[i];
+        V2 before{0, 0}, row{0, 0};
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const V2 t = s_row[i][w];
+            if (w < wave) before = before + t;
+            row = row + t;
+        }
+        const uint64_t f = base + (uint64_t)i * kBlock;
+        if (f < n) {
+            out_a[f] = run.a + before.a + ex[i].a;
+            out_b[f] = run.b + before.b + ex[i].b;
+        }
+        run = run + row;
     }
 }
 
@@ -216,19 +276,27 @@ __device__ __forceinline__ u32x4 byte_range(int lo, int hi)
                  dword_byte_mask(lo, hi, 3)};
 }
 
-// ------------------------------ frame-major mask-copy ------------------------------
+// ------------------------------ mask-copy ------------------------------
 // Output space [0, total) = regions back to back; region f = header (hl bytes,
-// 0 for a payload-only gather) then payload (len bytes) read from
-// src + descs[f].off and XORed with the rotated key.  Output words (16 B,
-// aligned) split into
-//   interior words: fully inside one payload -> interior_kernel, one wave per
-//     unit of 256 words (4 KiB), the source shift uniform per frame, so each
-//     lane loads one aligned word and takes the next from its neighbour;
-//   boundary words: the rest (a word whose first byte lies in a header, or
-//     the word straddling a payload end) -> boundary_kernel, owned by the one
-//     frame whose region holds the word's first byte, composed byte-exactly.
+// none for a payload-only gather) then payload (len bytes) read from
+// src + descs[f].off and XORed with the rotated key.
+//
+// Ownership: every 64-byte output granule belongs to the frame whose region
+// holds the granule's first byte.  A frame's owned granules are cut into wave
+// units of 256 words (4 KiB) whose bases are 1 KiB aligned, so a granule is
+// written by ONE store instruction of one wave (a line written piecewise by
+// different waves at different times -- e.g. a separate edge kernel -- goes to
+// memory as partial writes: unaligned units measured 15 % slower).  Only the line holding
+// a frame boundary is shared, by two adjacent units.  Inside a unit
+//   interior words (inside the frame's payload) take the fast path: the source
+//     shift is uniform, each lane loads one aligned word and takes the next one
+//     from its neighbour;
+//   edge words -- at most one holding the header's end, and the words after the
+//     payload's end up to the granule's end (the next frames' first bytes) --
+//     are composed byte-exactly beforehand by edge_kernel, one thread per word,
+//     into a per-frame buffer; the wave loads them (one lane per word) and moves
+//     them into their store lanes with a lane permute.
 // Every output byte in [0, total) is written exactly once.
-constexpr int kUnitWords = 256;  // interior words per wave unit (4 words per lane)
 
 struct FrameGeom {
     uint64_t r0, p0, r1;  // region start, payload start, region end (= payload end)
@@ -258,110 +326,273 @@ __device__ __forceinline__ FrameGeom geom(uint32_t f, const uint64_t* __restrict
     return g;
 }
 
-// Interior word range [wlo, whi) of a frame and its number of wave units.
-__device__ __forceinline__ void interior(const FrameGeom& g, uint64_t& wlo, uint64_t& whi)
-{
-    wlo = (g.p0 + 15) >> 4;
-    whi = g.r1 >> 4;
-    if (whi < wlo) whi = wlo;
-}
-
-template <bool HEADERS>
-struct UnitCount {
-    const uint64_t* start;
-    const kmws_desc* d;
-    const uint16_t* flags;
-    __device__ uint64_t operator()(uint32_t f) const
-    {
-        const FrameGeom g = geom<HEADERS>(f, start, d, flags);
-        uint64_t wlo, whi;
-        interior(g, wlo, whi);
-        return (whi - wlo + kUnitWords - 1) / kUnitWords;
-    }
+// Output words of a frame: owned [olo, ohi), interior [ilo, ihi) inside them,
+// and its units (bases b0, b0 + 256, ...).
+struct FrameWords {
+    uint64_t olo, ohi, ilo, ihi, b0, units;
 };
 
-// One record per interior unit, written by the unit's frame: everything a
-// wave needs in one 32-byte scalar load.
+__device__ __forceinline__ FrameWords frame_words(const FrameGeom& g, uint64_t total_words)
+{
+    FrameWords w;
+    w.olo = kLineWords * ((g.r0 + kLineBytes - 1) / kLineBytes);
+    uint64_t ohi = kLineWords * ((g.r1 + kLineBytes - 1) / kLineBytes);
+    if (ohi > total_words) ohi = total_words;  // the output's last line
+    w.ohi = ohi > w.olo ? ohi : w.olo;
+    uint64_t ilo = (g.p0 + 15) >> 4, ihi = g.r1 >> 4;  // words inside the payload
+    ilo = ilo > w.olo ? ilo : w.olo;
+    ihi = ihi < w.ohi ? ihi : w.ohi;
+    w.ilo = ilo < w.ohi ? ilo : w.ohi;
+    w.ihi = ihi > w.ilo ? ihi : w.ilo;
+    w.b0 = w.olo & ~(kUnitAlign - 1);
+    w.units = w.ohi > w.olo ? (w.ohi - w.b0 + kUnitWords - 1) / kUnitWords : 0;
+    return w;
+}
+
+// One record per unit slot: everything a wave needs in one 32-byte scalar load.
 struct UnitRec {
-    uint64_t dst;     // output byte of the unit's first word (16-B aligned)
-    uint64_t src;     // source byte of that word (any alignment)
-    uint32_t nwords;  // 1..kUnitWords
-    uint32_t rk;      // rotated key for the unit's aligned output words (0 = no mask)
-    uint64_t pad;
+    uint64_t dst;       // output byte of the unit's base word
+    uint64_t src;       // source byte of that word (any alignment)
+    uint32_t f;         // owning frame
+    uint32_t rk;        // rotated key for the unit's aligned output words (0 = no mask)
+    uint32_t own;       // owned words [klo, khi) of the unit: klo | head_f << 12 | khi << 16 (khi == 0:
+                        // empty slot); head_f = the frame's edge words before its interior
+    uint32_t inner;     // interior words [ilo, ihi): ilo | ihi << 16, klo <= ilo <= ihi <= khi
 };
 static_assert(sizeof(UnitRec) == 32, "UnitRec is one s_load_dwordx8");
 
-// Per-unit records; also the capacity check (status set if total > cap).
+// Adds frame h's bytes (header, then masked payload) that fall in [a, a + 16).
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __restrict__ start,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags,
-                                                          const uint64_t* __restrict__ unit_off, uint32_t n,
-                                                          uint64_t cap, UnitRec* __restrict__ rec,
-                                                          WsHead* __restrict__ head)
+__device__ __forceinline__ void add_frame(u32x4& out, uint64_t a, const FrameGeom& h, uint32_t fl,
+                                          const uint8_t* __restrict__ src)
 {
-    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    if (f >= n) return;
-    if (start[n] > cap) {
-        if (f == 0) atomicOr(&head->status, kStatusBadDesc);
-        return;
+    if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
+        uint64_t h0, h1;
+        build_header(h.len, fl, h.key, h0, h1);
+        const int s = (int)((int64_t)h.r0 - (int64_t)a);
+        const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+        const int he = (int)(h.p0 - h.r0) + s;
+        out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
     }
-    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
-    uint64_t wlo, whi;
-    interior(g, wlo, whi);
-    const uint32_t rk = g.key ? rot_key(g.key, g.p0) : 0u;
-    uint64_t w = wlo;
-    for (uint64_t u = unit_off[f]; u < unit_off[f + 1]; ++u, w += kUnitWords) {
-        UnitRec r;
-        r.dst = 16u * w;
-        r.src = 16u * w + g.sdel;
-        r.nwords = (uint32_t)(whi - w < (uint64_t)kUnitWords ? whi - w : (uint64_t)kUnitWords);
-        r.rk = rk;
-        r.pad = 0;
-        rec[u] = r;
+    if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
+        const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+        const uint64_t slo = lo_b + h.sdel, shi = hi_b + h.sdel;
+        const uint64_t s0 = slo & ~(uint64_t)15, s1 = (shi - 1) & ~(uint64_t)15;
+        const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + s0);
+        const u32x4 W1 = s1 != s0 ? *reinterpret_cast<const u32x4*>(src + s1) : W0;
+        const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
+        const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd)
+                                : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
+        const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
+        out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
     }
 }
 
-// One wave per interior unit: 4 words per lane, 1 KiB per wave-instruction.
-__global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                          const uint64_t* __restrict__ unit_off, uint32_t n,
-                                                          const UnitRec* __restrict__ rec,
-                                                          const WsHead* __restrict__ head, uint64_t unit_base)
+// Output word [a, a + 16) composed from every frame from f on that overlaps it.
+// A word overlaps frames f, f+1, f+2 in all but tiny-frame batches: their
+// geometry is loaded at once (one latency level), any further frames one by one.
+template <bool HEADERS>
+__device__ u32x4 compose_word(uint64_t a, uint32_t f, uint32_t n, const uint8_t* __restrict__ src,
+                              const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
+                              const uint16_t* __restrict__ flags)
+{
+    constexpr int kPre = 3;
+    FrameGeom g[kPre];
+    uint32_t fl[kPre];
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+        const uint32_t j = f + i;
+        if (j < n) {
+            g[i] = geom<HEADERS>(j, start, d, flags);
+            fl[i] = HEADERS ? flags[j] : 0u;
+        } else {
+            g[i].r0 = ~0ull;  // past the last frame: overlaps nothing
+            fl[i] = 0;
+        }
+    }
+    u32x4 out = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < kPre; ++i)
+        if (g[i].r0 < a + 16) add_frame<HEADERS>(out, a, g[i], fl[i], src);
+    if (g[kPre - 1].r0 < a + 16) {
+        for (uint32_t j = f + kPre; j < n; ++j) {
+            const FrameGeom h = geom<HEADERS>(j, start, d, flags);
+            if (h.r0 >= a + 16) break;
+            add_frame<HEADERS>(out, a, h, HEADERS ? flags[j] : 0u, src);
+        }
+    }
+    return out;
+}
+
+// Unit records of 256 frames per block, written slot by slot (coalesced): each
+// slot finds its frame by a binary search over the block's slot bases in LDS.
+// Frame f owns slots [ubase[f], ubase[f+1]); slots past its exact unit count
+// are marked empty.  Also the capacity check (status set if total > cap).
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __restrict__ start,
+                                                          const uint64_t* __restrict__ ubase,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          uint64_t cap, UnitRec* __restrict__ rec,
+                                                          WsHead* __restrict__ head)
+{
+    __shared__ uint32_t s_ub[kBlock + 1];
+    const uint32_t f0 = blockIdx.x * kBlock;
+    const uint64_t total = start[n];
+    if (total > cap) {  // records would not fit the workspace; the copy waves see the status
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    const uint32_t nf = n - f0 < (uint32_t)kBlock ? n - f0 : (uint32_t)kBlock;
+    const uint64_t S0 = ubase[f0];
+    if (threadIdx.x < nf) s_ub[threadIdx.x] = (uint32_t)(ubase[f0 + threadIdx.x] - S0);
+    if (threadIdx.x == 0) s_ub[nf] = (uint32_t)(ubase[f0 + nf] - S0);  // nf may be kBlock
+    __syncthreads();
+    const uint32_t ns = s_ub[nf];
+    const uint64_t total_words = (total + 15) >> 4;
+    for (uint32_t s = threadIdx.x; s < ns; s += kBlock) {
+        uint32_t lo = 0, hi = nf;  // s_ub[lo] <= s < s_ub[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_ub[mid] <= s) lo = mid; else hi = mid;
+        }
+        const uint32_t f = f0 + lo;
+        const uint64_t m = s - s_ub[lo];
+        const FrameGeom g = geom<HEADERS>(f, start, d, flags);
+        const FrameWords w = frame_words(g, total_words);
+        UnitRec r;
+        if (m < w.units) {
+            const uint64_t b = w.b0 + m * kUnitWords;
+            auto rel = [&](uint64_t x) -> uint32_t {
+                return (uint32_t)(x <= b ? 0 : (x - b >= (uint64_t)kUnitWords ? kUnitWords : x - b));
+            };
+            r.dst = 16u * b;
+            r.src = 16u * b + g.sdel;
+            r.f = f;
+            r.rk = g.key ? rot_key(g.key, g.p0) : 0u;
+            const uint32_t klo = rel(w.olo), khi = rel(w.ohi), ilo = rel(w.ilo), ihi = rel(w.ihi);
+            const uint32_t head_f = (uint32_t)(w.ilo - w.olo);
+            r.own = klo | head_f << 12 | khi << 16;
+            r.inner = ilo | ihi << 16;
+            if (head_f + (khi - ihi) > (uint32_t)kEdgeWords || ilo - klo > head_f)  // cannot happen
+                atomicOr(&head->status, kStatusBadDesc);
+        } else {
+            r.dst = r.src = 0;
+            r.f = r.rk = 0;
+            r.own = r.inner = 0;
+        }
+        rec[S0 + s] = r;
+    }
+}
+
+// A frame's edge words -- its owned words outside its interior: q < head_f at
+// olo + q, then the tail at ihi + (q - head_f) -- composed one thread per
+// (frame, q) into edge[f * kEdgeWords + q].
+constexpr int kEdgeFramesPerBlock = kBlock / kEdgeWords;  // 28 frames, 252 threads
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) edge_kernel(const uint8_t* __restrict__ src,
+                                                      const uint64_t* __restrict__ start,
+                                                      const kmws_desc* __restrict__ d,
+                                                      const uint16_t* __restrict__ flags, uint32_t n,
+                                                      uint64_t cap, u32x4* __restrict__ edge,
+                                                      const WsHead* __restrict__ head, uint64_t block_base)
+{
+    const uint32_t t = threadIdx.x;
+    const uint64_t f64 = (block_base + blockIdx.x) * kEdgeFramesPerBlock + t / kEdgeWords;
+    if (t >= (uint32_t)(kEdgeFramesPerBlock * kEdgeWords) || f64 >= n) return;
+    const uint64_t total = start[n];
+    if (total > cap || head->status != 0) return;
+    const uint32_t f = (uint32_t)f64, q = t % kEdgeWords;
+    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
+    const FrameWords w = frame_words(g, (total + 15) >> 4);
+    const uint64_t head_f = w.ilo - w.olo, tail = w.ohi - w.ihi;
+    uint64_t word;
+    if (q < head_f) word = w.olo + q;
+    else if (q < head_f + tail) word = w.ihi + (q - head_f);
+    else return;
+    edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, src, start, d, flags);
+}
+
+__device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
+{
+    return u32x4{(uint32_t)__shfl((int)v.x, lane, 64), (uint32_t)__shfl((int)v.y, lane, 64),
+                 (uint32_t)__shfl((int)v.z, lane, 64), (uint32_t)__shfl((int)v.w, lane, 64)};
+}
+
+// One wave per unit: 4 words per lane, 1 KiB per wave-instruction.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                      const uint64_t* __restrict__ start,
+                                                      const kmws_desc* __restrict__ d,
+                                                      const uint16_t* __restrict__ flags, uint32_t n,
+                                                      const uint64_t* __restrict__ ubase,
+                                                      const UnitRec* __restrict__ rec,
+                                                      const u32x4* __restrict__ edge,
+                                                      const WsHead* __restrict__ head, uint64_t unit_base)
 {
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: provably uniform, so the record is one scalar load
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t u = unit_base + (uint64_t)blockIdx.x * (kBlock / 64) + wave;
-    // record, unit count and status are independent scalar loads (one latency
-    // level); records past the count lie inside the workspace and are ignored
+    // record, slot count, status and total are independent scalar loads (one
+    // latency level); slots past the count lie inside the workspace and are ignored
     const UnitRec r = rec[u];
-    const uint64_t total_units = unit_off[n];
+    const uint64_t total_units = ubase[n];
     const uint32_t st = head->status;
+    const uint64_t total = start[n];
     // no early exit between these loads and their uses (the compiler would sink
-    // the record load below the count's wait): an out-of-range wave has 0 words
-    const uint32_t nwords = (u < total_units && st == 0) ? r.nwords : 0u;
-    const uint32_t delta = (uint32_t)(r.src & 15u);   // same for every word of the unit
-    if (nwords == 0) return;                            // wave-uniform, after the record's wait
+    // the record load below the count's wait): an out-of-range wave owns no words
+    const uint32_t khi = (u < total_units && st == 0) ? r.own >> 16 : 0u;
+    // keep every field's load above the exit (one wait for all of them)
+    asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
+    if (khi == 0) return;  // wave-uniform, after the record's wait
+    const uint32_t klo = r.own & 0x1FFu, head_f = (r.own >> 12) & 0xFu;
+    const uint32_t ilo = r.inner & 0xFFFFu, ihi = r.inner >> 16;
+    const uint32_t delta = (uint32_t)(r.src & 15u);  // same for every word of the unit
     const uint8_t* s0 = src + (r.src - delta);
-    const uint32_t last = nwords - 1;
     constexpr int kW = kUnitWords / 64;
     // Every load is issued before the first store (vmcnt also counts stores, so
     // a load issued after a store would make its wait cover that store too).
-    // Addresses are clamped to the unit instead of predicating the loads.
+    // Fast-path addresses are clamped to [ilo, ihi - 1] instead of predicating.
+    const bool fast = ihi > ilo;
+    const uint32_t last = fast ? ihi - 1 : ilo;
     u32x4 lo[kW], ex[kW];
+    if (!fast) {
 #pragma unroll
-    for (int i = 0; i < kW; ++i) {
-        const uint32_t k = lane + 64 * i;
-        lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * (k < last ? k : last)));
-    }
-    if (delta) {
-        // the next aligned source word comes from lane + 1, except on lane 63
-        // and on the unit's last word, which load it themselves
+        for (int i = 0; i < kW; ++i) lo[i] = u32x4{0, 0, 0, 0};
+    } else {
 #pragma unroll
         for (int i = 0; i < kW; ++i) {
             const uint32_t k = lane + 64 * i;
-            if (lane == 63 || k >= last)
-                ex[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * ((k < last ? k : last) + 1));
+            const uint32_t kk = k < ilo ? ilo : (k < last ? k : last);
+            lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * kk));
+        }
+        if (delta) {
+            // the next aligned source word comes from lane + 1, except on lane 63
+            // and on the last interior word, which load it themselves
+#pragma unroll
+            for (int i = 0; i < kW; ++i) {
+                const uint32_t k = lane + 64 * i;
+                if (lane == 63 || k >= last)
+                    ex[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * ((k < last ? k : last) + 1));
+            }
+        }
+    }
+    // Edge words (composed by unit_rec): [klo, ilo) then [ihi, khi), one per lane.
+    const uint32_t nhead = ilo - klo, nslow = nhead + (khi - ihi);
+    u32x4 sv = u32x4{0, 0, 0, 0};
+    if (nslow && lane < (int)nslow) {
+        const uint32_t q = (uint32_t)lane < nhead ? lane : head_f + (lane - nhead);
+        sv = edge[(uint64_t)r.f * kEdgeWords + q];
+        const uint32_t k = (uint32_t)lane < nhead ? klo + lane : ihi + (lane - nhead);
+        const uint64_t a = r.dst + 16u * k;
+        if (a + 16 > total) {  // the output's last, partial word: byte stores
+#pragma clang loop vectorize(disable) unroll(disable)
+            for (uint64_t p = a; p < total; ++p) {
+                const uint32_t b = (uint32_t)(p - a);
+                const uint32_t v = (b & 8u) ? ((b & 4u) ? sv.w : sv.z) : ((b & 4u) ? sv.y : sv.x);
+                dst[p] = (uint8_t)(v >> (8 * (b & 3u)));
+            }
         }
     }
     u32x4 out[kW];
@@ -369,7 +600,7 @@ __global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restr
     for (int i = 0; i < kW; ++i) {
         const uint32_t k = lane + 64 * i;
         u32x4 v = lo[i];
-        if (delta) {
+        if (fast && delta) {
             u32x4 hi;
             hi.x = __shfl_down(lo[i].x, 1, 64);
             hi.y = __shfl_down(lo[i].y, 1, 64);
@@ -379,70 +610,21 @@ __global__ void __launch_bounds__(kBlock) interior_kernel(const uint8_t* __restr
             v = funnel16(lo[i], hi, delta);
         }
         out[i] = v ^ r.rk;
+        // composed words of this instruction's 64 (wave-uniform test)
+        const uint32_t c0 = 64u * i, c1 = c0 + 64u;
+        if ((klo < ilo && klo < c1 && ilo > c0) || (ihi < khi && ihi < c1 && khi > c0)) {
+            const bool slow = (k >= klo && k < ilo) || (k >= ihi && k < khi);
+            const int from = (int)(k < ilo ? k - klo : nhead + (k - ihi)) & 63;
+            const u32x4 w = shfl16(sv, from);
+            if (slow) out[i] = w;
+        }
     }
 #pragma unroll
     for (int i = 0; i < kW; ++i) {
         const uint32_t k = lane + 64 * i;
-        if (k < nwords) __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + r.dst + 16u * k));
-    }
-}
-
-// One lane per frame: the boundary words whose first byte lies in this frame's
-// region: [ceil(r0/16), ceil(p0/16)) (header words) and the word straddling the
-// payload end, composed from every frame that overlaps them.
-template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) boundary_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                          const uint64_t* __restrict__ start,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags, uint32_t n,
-                                                          const WsHead* __restrict__ head)
-{
-    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    if (f >= n || head->status != 0) return;
-    const uint64_t total = start[n];
-    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
-    const uint64_t a_hdr0 = (g.r0 + 15) >> 4, a_hdr1 = (g.p0 + 15) >> 4;
-    const uint64_t b0 = (g.r1 >> 4) > a_hdr1 ? (g.r1 >> 4) : a_hdr1, b1 = (g.r1 + 15) >> 4;
-    for (int part = 0; part < 2; ++part) {
-        const uint64_t wa = part == 0 ? a_hdr0 : b0, wb = part == 0 ? a_hdr1 : b1;
-        for (uint64_t w = wa; w < wb; ++w) {
-            const uint64_t a = 16u * w;
-            u32x4 out = u32x4{0, 0, 0, 0};
-            for (uint32_t j = f; j < n; ++j) {
-                const FrameGeom h = j == f ? g : geom<HEADERS>(j, start, d, flags);
-                if (h.r0 >= a + 16) break;
-                if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
-                    const kmws_desc x = d[j];
-                    uint64_t h0, h1;
-                    build_header(x.len, flags[j], x.key, h0, h1);
-                    const int s = (int)((int64_t)h.r0 - (int64_t)a);
-                    const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                    const int he = (int)(h.p0 - h.r0) + s;
-                    out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
-                }
-                if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
-                    const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
-                    const uint64_t slo = lo_b + h.sdel, shi = hi_b + h.sdel;
-                    const uint64_t s0 = slo & ~(uint64_t)15, s1 = (shi - 1) & ~(uint64_t)15;
-                    const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + s0);
-                    const u32x4 W1 = s1 != s0 ? *reinterpret_cast<const u32x4*>(src + s1) : W0;
-                    const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
-                    const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd)
-                                            : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
-                    const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
-                    out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
-                }
-            }
-            if (a + 16 <= total) {
-                *reinterpret_cast<u32x4*>(dst + a) = out;
-            } else {  // last partial word of the output: byte stores
-                for (uint64_t p = a; p < total; ++p) {
-                    const uint32_t k = (uint32_t)(p - a);
-                    const uint32_t dwv = (k & 8u) ? ((k & 4u) ? out.w : out.z) : ((k & 4u) ? out.y : out.x);
-                    dst[p] = (uint8_t)(dwv >> (8 * (k & 3u)));
-                }
-            }
-        }
+        const uint64_t a = r.dst + 16u * k;
+        if (k >= klo && k < khi && a + 16 <= total)
+            __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + a));
     }
 }
 
@@ -529,19 +711,26 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
 // ------------------------------ host launchers ------------------------------
 struct CopyWs {
     WsHead* head;
-    uint64_t* partials;
-    uint64_t* unit_off;
+    V2* partials;
+    uint64_t* ubase;
     UnitRec* rec;
+    u32x4* edge;
 };
 
 static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
-static uint64_t max_units(uint32_t n, uint64_t cap) { return (cap + kUnitWords * 16 - 1) / (kUnitWords * 16) + n; }
+// sum of unit_bound(R_f) <= total / 4096 + 1.25 n (and total <= cap)
+// (rounded up to whole blocks: every wave of the copy grid reads its record)
+static uint64_t max_units(uint32_t n, uint64_t cap)
+{
+    const uint64_t u = (cap + kUnitWords * 16 - 1) / (kUnitWords * 16) + 2ull * n;
+    return (u + kBlock / 64 - 1) / (kBlock / 64) * (kBlock / 64);
+}
 static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * 8) + r16(((uint64_t)n + 1) * 8) +
-           max_units(n, cap) * sizeof(UnitRec);
+    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8) +
+           (uint64_t)n * kEdgeWords * 16 + max_units(n, cap) * sizeof(UnitRec);
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -550,22 +739,28 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     char* p = static_cast<char*>(ws);
     c.head = reinterpret_cast<WsHead*>(p);
     p += sizeof(WsHead);
-    c.partials = reinterpret_cast<uint64_t*>(p);
-    p += r16((n_scan_blocks(n) + 1) * 8);
-    c.unit_off = reinterpret_cast<uint64_t*>(p);
+    c.partials = reinterpret_cast<V2*>(p);
+    p += r16((n_scan_blocks(n) + 1) * sizeof(V2));
+    c.ubase = reinterpret_cast<uint64_t*>(p);
     p += r16(((uint64_t)n + 1) * 8);
+    c.edge = reinterpret_cast<u32x4*>(p);
+    p += (uint64_t)n * kEdgeWords * 16;
     c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
 }
 
+// Region offsets -> out (n+1 entries), unit slot bases -> c.ubase (n+1 entries).
 template <class Size>
-static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, uint64_t* partials, hipStream_t s)
+static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s)
 {
     const uint32_t nb = (uint32_t)n_scan_blocks(n);
-    if (nb == 0) return hip_status(hipMemsetAsync(out, 0, sizeof(uint64_t), s));
-    hipLaunchKernelGGL(scan_reduce_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, partials);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kBlock), 0, s, partials, nb, out + n);
-    hipLaunchKernelGGL(scan_emit_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, partials, out);
+    if (nb == 0) {
+        if (hipMemsetAsync(out, 0, sizeof(uint64_t), s) != hipSuccess) return KMWS_ERR_FAILED;
+        return hip_status(hipMemsetAsync(c.ubase, 0, sizeof(uint64_t), s));
+    }
+    hipLaunchKernelGGL(scan_reduce_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kBlock), 0, s, c.partials, nb, out + n, c.ubase + n);
+    hipLaunchKernelGGL(scan_emit_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials, out, c.ubase);
     return hip_status(hipGetLastError());
 }
 
@@ -573,20 +768,32 @@ template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, const uint64_t* start,
                                const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
-    kmws_status st = launch_scan(UnitCount<HEADERS>{start, d, flags}, n, c.unit_off, c.partials, s);
-    if (st != KMWS_OK) return st;
     const uint32_t fb = (n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(unit_rec_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, start, d, flags, c.unit_off, n, cap,
+    hipLaunchKernelGGL(unit_rec_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, start, c.ubase, d, flags, n, cap,
                        c.rec, c.head);
+    const uint64_t eb = ((uint64_t)n + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
+    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;  // stay below 2^32 work-items per launch
+    for (uint64_t b0 = 0; b0 < eb; b0 += kMaxBlocks)
+        hipLaunchKernelGGL(edge_kernel<HEADERS>, dim3((uint32_t)(eb - b0 < kMaxBlocks ? eb - b0 : kMaxBlocks)),
+                           dim3(kBlock), 0, s, src, start, d, flags, n, cap, c.edge, c.head, b0);
+    // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
+    // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
+    // batches of small frames need every wave slot to hide their per-unit
+    // latency.  cap / n bounds the mean region size from above.
+    // KMWS_COPY_LDS_PAD overrides the LDS bytes per block (tuning).
+    static const int lds_env = [] {
+        const char* e = getenv("KMWS_COPY_LDS_PAD");
+        return e ? atoi(e) : -1;
+    }();
+    const unsigned lds_pad = lds_env >= 0 ? (unsigned)lds_env : (cap / n >= 16384 ? 32768u : 0u);
     const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
     constexpr uint64_t kWavesPerBlock = kBlock / 64;
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
     for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
         const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
-        hipLaunchKernelGGL(interior_kernel, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kBlock), 0, s, src, dst, c.unit_off, n, c.rec, c.head, u0);
+        hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0);
     }
-    hipLaunchKernelGGL(boundary_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, src, dst, start, d, flags, n, c.head);
     return hip_status(hipGetLastError());
 }
 
@@ -609,7 +816,7 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
     if (hipMemsetAsync(c.head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
-    kmws_status st = launch_scan(WireSize{descs, flags}, n, wire_off, c.partials, s);
+    kmws_status st = launch_scan(WireSize{descs, flags}, n, wire_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<true>(src, dst, dst_cap, wire_off, descs, flags, n, c, s);
 }
@@ -625,7 +832,7 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
     if (hipMemsetAsync(c.head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
-    kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c.partials, s);
+    kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
