@@ -388,32 +388,81 @@ __device__ __forceinline__ void add_frame(u32x4& out, uint64_t a, const FrameGeo
     }
 }
 
-// Output word [a, a + 16) composed from every frame from f on that overlaps it.
-// A word overlaps frames f, f+1, f+2 in all but tiny-frame batches: their
-// geometry is loaded at once (one latency level), any further frames one by one.
+// Geometry (and flags) of frames f, f+1, f+2 -- the frames a word starting in
+// frame f overlaps in all but tiny-frame batches -- loaded at once (indices
+// clamped instead of branches, so the loads issue together).
+constexpr int kPre = 3;
 template <bool HEADERS>
-__device__ u32x4 compose_word(uint64_t a, uint32_t f, uint32_t n, const uint8_t* __restrict__ src,
+__device__ __forceinline__ void load_geoms(uint32_t f, uint32_t n, FrameGeom (&g)[kPre], uint32_t (&fl)[kPre],
+                                           const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
+                                           const uint16_t* __restrict__ flags)
+{
+    kmws_desc x[kPre];
+    uint64_t r0[kPre];
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {  // every load first, then the arithmetic
+        const uint32_t j = f + i < n ? f + i : n - 1;
+        x[i] = d[j];
+        r0[i] = start[j];
+        fl[i] = HEADERS ? flags[j] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+        const uint32_t mask = HEADERS ? (fl[i] >> 8) & 1u : 1u;
+        const uint32_t hl = HEADERS ? hdr_len(x[i].len, mask) : 0u;
+        g[i].r0 = f + i < n ? r0[i] : ~0ull;  // past the last frame: overlaps nothing
+        g[i].p0 = r0[i] + hl;
+        g[i].r1 = g[i].p0 + x[i].len;
+        g[i].sdel = x[i].off - g[i].p0;
+        g[i].key = mask ? x[i].key : 0u;
+        g[i].len = x[i].len;
+    }
+}
+
+// Output word [a, a + 16) composed from every frame from f on that overlaps it
+// (g, fl: load_geoms(f)).  The payload source words of the three frames are
+// loaded together (src + 0 where a frame has none); frames past f+2 are
+// walked one by one.
+template <bool HEADERS>
+__device__ u32x4 compose_word(uint64_t a, uint32_t f, uint32_t n, const FrameGeom (&g)[kPre],
+                              const uint32_t (&fl)[kPre], const uint8_t* __restrict__ src,
                               const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
                               const uint16_t* __restrict__ flags)
 {
-    constexpr int kPre = 3;
-    FrameGeom g[kPre];
-    uint32_t fl[kPre];
+    u32x4 W0[kPre], W1[kPre];
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
-        const uint32_t j = f + i;
-        if (j < n) {
-            g[i] = geom<HEADERS>(j, start, d, flags);
-            fl[i] = HEADERS ? flags[j] : 0u;
-        } else {
-            g[i].r0 = ~0ull;  // past the last frame: overlaps nothing
-            fl[i] = 0;
-        }
+        const FrameGeom& h = g[i];
+        const bool pay = h.r0 < a + 16 && h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a;
+        const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+        const uint64_t s0 = pay ? (lo_b + h.sdel) & ~(uint64_t)15 : 0;
+        const uint64_t s1 = pay ? (hi_b + h.sdel - 1) & ~(uint64_t)15 : 0;
+        W0[i] = *reinterpret_cast<const u32x4*>(src + s0);
+        W1[i] = *reinterpret_cast<const u32x4*>(src + s1);
     }
     u32x4 out = u32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < kPre; ++i)
-        if (g[i].r0 < a + 16) add_frame<HEADERS>(out, a, g[i], fl[i], src);
+    for (int i = 0; i < kPre; ++i) {
+        const FrameGeom& h = g[i];
+        if (h.r0 >= a + 16) continue;
+        if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
+            uint64_t h0, h1;
+            build_header(h.len, fl[i], h.key, h0, h1);
+            const int s = (int)((int64_t)h.r0 - (int64_t)a);
+            const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+            const int he = (int)(h.p0 - h.r0) + s;
+            out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
+        }
+        if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
+            const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+            const uint64_t s0 = (lo_b + h.sdel) & ~(uint64_t)15;
+            const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
+            const u32x4 V = dd >= 0 ? funnel16(W0[i], W1[i], (uint32_t)dd)
+                                    : funnel16(u32x4{0, 0, 0, 0}, W0[i], (uint32_t)(16 + dd));
+            const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
+            out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
+        }
+    }
     if (g[kPre - 1].r0 < a + 16) {
         for (uint32_t j = f + kPre; j < n; ++j) {
             const FrameGeom h = geom<HEADERS>(j, start, d, flags);
@@ -500,17 +549,21 @@ __global__ void __launch_bounds__(kBlock) edge_kernel(const uint8_t* __restrict_
     const uint32_t t = threadIdx.x;
     const uint64_t f64 = (block_base + blockIdx.x) * kEdgeFramesPerBlock + t / kEdgeWords;
     if (t >= (uint32_t)(kEdgeFramesPerBlock * kEdgeWords) || f64 >= n) return;
-    const uint64_t total = start[n];
-    if (total > cap || head->status != 0) return;
     const uint32_t f = (uint32_t)f64, q = t % kEdgeWords;
-    const FrameGeom g = geom<HEADERS>(f, start, d, flags);
-    const FrameWords w = frame_words(g, (total + 15) >> 4);
+    // total, status and the three frames' geometry: one latency level
+    const uint64_t total = start[n];
+    const uint32_t st = head->status;
+    FrameGeom g[kPre];
+    uint32_t fl[kPre];
+    load_geoms<HEADERS>(f, n, g, fl, start, d, flags);
+    if (total > cap || st != 0) return;
+    const FrameWords w = frame_words(g[0], (total + 15) >> 4);
     const uint64_t head_f = w.ilo - w.olo, tail = w.ohi - w.ihi;
     uint64_t word;
     if (q < head_f) word = w.olo + q;
     else if (q < head_f + tail) word = w.ihi + (q - head_f);
     else return;
-    edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, src, start, d, flags);
+    edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, g, fl, src, start, d, flags);
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
