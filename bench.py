@@ -88,11 +88,11 @@ def _cpu_model() -> str:
 
 def traffic_from_profile(frames: int, frame_len: int, kernel: str):
     """HBM bytes per launch of the unmask kernel from the committed PMC pass
-    (profiles/*_traffic.json, written by tools/pmc_traffic.py), if it was
+    (profiles/*traffic*.json, written by tools/pmc_traffic.py), if it was
     measured on this exact configuration; else None."""
     import glob
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
