@@ -86,6 +86,20 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def schedule_kernel(schedule: int) -> str:
+    """Kernel that carries the unmask for a kmws_unmask_schedule() code."""
+    if schedule == 0:
+        return "unmask_tiles_kernel"
+    return "unmask_pipe_kernel" if schedule & 1 else "unmask_persist_kernel"
+
+
+def schedule_name(schedule: int) -> str:
+    if schedule == 0:
+        return "one block per 16 KiB tile"
+    kind = "pipelined persistent grid" if schedule & 1 else "persistent grid-stride"
+    return f"{kind}, {schedule & ~1} blocks (autotuned)"
+
+
 def traffic_from_profile(frames: int, frame_len: int, kernel: str):
     """HBM bytes per launch of the unmask kernel from the committed PMC pass
     (profiles/*traffic*.json, written by tools/pmc_traffic.py), if it was
@@ -201,7 +215,7 @@ def main():
     value = shard.aggregate_rate([span * a.steps] * world, [elapsed] * world) / 2**30
     alg_bytes = n * (2 * L + DESC_BYTES)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profile(n, L, "unmask_tiles_kernel" if schedule == 0 else "unmask_persist_kernel")
+    traffic = traffic_from_profile(n, L, schedule_kernel(schedule))
 
     out = None
     if rank == 0:
@@ -220,12 +234,11 @@ def main():
                        "layout": "aligned arena, frame i at i*frame_len",
                        "parallelism": f"frame-partition x{world} (no collective)",
                        "tile_variant": "default" if variant is None else variant,
-                       "unmask_schedule": "one block per 16 KiB tile" if schedule == 0 else
-                                          f"persistent grid-stride, {schedule} blocks (autotuned)"},
+                       "unmask_schedule": schedule_name(schedule)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "unmask_tiles_kernel" if schedule == 0 else "unmask_persist_kernel",
+                         "kernel": schedule_kernel(schedule),
                          "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /

@@ -180,18 +180,22 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
                               const void* workspace, size_t workspace_bytes, void* stream);
 
 /* Optional one-time tuning (like a cuDNN benchmark pass): runs each unmask
- * schedule -- one block per tile, or a persistent grid-stride grid -- twice
+ * schedule -- one block per tile, a persistent grid-stride grid, or a
+ * software-pipelined persistent grid -- twice
  * on this batch (the XOR applied twice leaves the payload unchanged), times
  * them with events on `stream` (synchronizes) and makes the fastest the
  * current device's schedule for kmws_unmask_apply / kmws_unmask_batch.
- * Returns the chosen schedule (0 = one block per tile, else grid size) or a
- * negative status.  kmws_unmask_schedule() reports the current one. */
+ * Returns the chosen schedule (0 = one block per tile; else the grid size,
+ * plus 1 for the pipelined grid) or a negative status.  kmws_unmask_schedule() reports the current one. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
 int kmws_unmask_schedule(void);
 
 /* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2);
- * 16 KiB tiles on a persistent grid-stride grid of 4096 (3), 6144 (4) or 8192 (5) blocks. */
+ * 16 KiB tiles on a persistent grid-stride grid of 8 K (3), 16 K (4), 24 K (5),
+ * 32 K (6) or 64 K (7) blocks; one block per tile with registers capped for 6 (8)
+ * or 8 (9) waves per SIMD; pipelined persistent grid of 16 K (10), 32 K (11) or
+ * 64 K (12) blocks. */
 kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       void* workspace, size_t workspace_bytes, void* stream, int variant);
 

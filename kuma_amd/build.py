@@ -34,25 +34,28 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Compiles the library; `out` + `defines` (-D flags) make a tuning variant
+    (tools/ab_pack.py) without touching the product library."""
+    if out is None and not force and up_to_date():
         return LIB
+    lib = out or LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     objs = []
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
     for src in sources():
-        obj = os.path.join(LIB_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(LIB_DIR, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
         cmd = ["hipcc", "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-Wall", "-Wno-unused-function", *inc, "-c", src, "-o", obj]
+               "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *inc, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib]
     subprocess.check_call(cmd)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -77,7 +77,13 @@ struct V2 {
 };
 __device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b + y.b}; }
 
-constexpr int kUnitWords = 256;   // output words per wave unit (4 per lane)
+#ifndef KMWS_UNIT_LANE_WORDS
+#define KMWS_UNIT_LANE_WORDS 4
+#endif
+// Output words per wave unit: 4 per lane (4 KiB).  2, 3, 5, 6 and 8 words per
+// lane measured the same or slower on cfg3/cfg4/64 KiB frames (within the
+// +-4 % run-to-run spread of one box; tools/gpu_ab_units.sh).
+constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
 constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
 #ifndef KMWS_LINE_BYTES
 #define KMWS_LINE_BYTES 64
@@ -283,7 +289,7 @@ __device__ __forceinline__ u32x4 byte_range(int lo, int hi)
 //
 // Ownership: every 64-byte output granule belongs to the frame whose region
 // holds the granule's first byte.  A frame's owned granules are cut into wave
-// units of 256 words (4 KiB) whose bases are 1 KiB aligned, so a granule is
+// units of kUnitWords words (4 KiB) whose bases are 1 KiB aligned, so a granule is
 // written by ONE store instruction of one wave (a line written piecewise by
 // different waves at different times -- e.g. a separate edge kernel -- goes to
 // memory as partial writes: unaligned units measured 15 % slower).  Only the line holding
@@ -572,7 +578,138 @@ __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
                  (uint32_t)__shfl((int)v.z, lane, 64), (uint32_t)__shfl((int)v.w, lane, 64)};
 }
 
-// One wave per unit: 4 words per lane, 1 KiB per wave-instruction.
+// A unit's record decoded into wave-uniform scalars.
+struct UnitInfo {
+    uint64_t dst;       // output byte of the unit's base word
+    const uint8_t* s0;  // aligned source word of the base word
+    uint32_t f, rk, delta, klo, khi, ilo, ihi, head_f, last;
+    bool fast;          // the unit has interior words
+};
+
+__device__ __forceinline__ UnitInfo decode_unit(const UnitRec& r, bool live, const uint8_t* __restrict__ src)
+{
+    UnitInfo x;  // a dead unit (past the count, or a bad batch) owns, loads and stores nothing
+    const uint32_t own = live ? r.own : 0u, inner = live ? r.inner : 0u;
+    x.khi = own >> 16;
+    x.klo = own & 0x1FFu;
+    x.head_f = (own >> 12) & 0xFu;
+    x.ilo = inner & 0xFFFFu;
+    x.ihi = inner >> 16;
+    x.delta = (uint32_t)(r.src & 15u);  // same for every word of the unit
+    x.s0 = src + (r.src - x.delta);
+    x.dst = r.dst;
+    x.f = live ? r.f : 0u;
+    x.rk = r.rk;
+    x.fast = x.ihi > x.ilo;
+    x.last = x.fast ? x.ihi - 1 : x.ilo;
+    return x;
+}
+
+constexpr int kUnitW = kUnitWords / 64;  // words per lane
+struct UnitRegs {
+    u32x4 lo[kUnitW];  // aligned source word of each of the lane's output words
+    u32x4 ex;          // the source word after the last interior word (every lane: one address)
+    u32x4 sv;          // this lane's edge word, if any
+};
+
+// Issues every load of a unit, and nothing else, in straight-line code (no
+// branch around a load: the wait before the unit's stores then counts exactly
+// the loads issued after them, so a later unit's loads could stay in flight
+// unit's loads in flight).  Interior words: one aligned source word per lane,
+// addresses clamped to [ilo, ihi - 1] (a unit without interior words reads
+// src's first word instead); the next source word comes from the neighbour
+// lane, lane 63 takes it from lane 0 of the next instruction, and the last
+// interior word from `ex`.  Edge words (composed by edge_kernel: [klo, ilo)
+// then [ihi, khi)): one per lane, index clamped.
+__device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const uint8_t* __restrict__ src,
+                                           const u32x4* __restrict__ edge, UnitRegs& R)
+{
+    const uint8_t* s0 = x.fast ? x.s0 : src;
+    const uint32_t lo_k = x.fast ? x.ilo : 0u, hi_k = x.fast ? x.last : 0u;
+#pragma unroll
+    for (int i = 0; i < kUnitW; ++i) {
+        const uint32_t k = lane + 64 * i;
+        const uint32_t kk = k < lo_k ? lo_k : (k < hi_k ? k : hi_k);
+        R.lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * kk));
+    }
+    // word last + 1 holds payload bytes only when the source is shifted (delta != 0)
+    uint32_t xk = x.fast && x.delta ? x.last + 1 : hi_k;
+    asm("" : "+v"(xk));  // a vector load (a uniform address would become a scalar load: lgkmcnt)
+    R.ex = *reinterpret_cast<const u32x4*>(s0 + 16u * xk);
+    const uint32_t nhead = x.ilo - x.klo;
+    uint32_t q = (uint32_t)lane < nhead ? lane : x.head_f + (lane - nhead);
+    q = q < (uint32_t)kEdgeWords ? q : (uint32_t)kEdgeWords - 1;
+    R.sv = edge[(uint64_t)x.f * kEdgeWords + q];
+}
+
+__device__ __forceinline__ u32x4 readlane0(const u32x4& v)
+{
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0), (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0)};
+}
+
+// Composes and stores a unit whose loads unit_issue issued: every owned word of
+// the unit, each 64-byte granule by one store instruction.
+__device__ __forceinline__ void unit_finish(const UnitInfo& x, int lane, uint8_t* __restrict__ dst, uint64_t total,
+                                            const UnitRegs& R)
+{
+    // Every register the unit loaded is consumed here on every path, so the wait
+    // for them is a counted one and no load into these registers stays pending
+    // (a pending one would force a full wait before the registers are reused).
+#pragma unroll
+    for (int i = 0; i < kUnitW; ++i) asm volatile("" ::"v"(R.lo[i]));
+    asm volatile("" ::"v"(R.ex), "v"(R.sv));
+    const uint32_t nhead = x.ilo - x.klo, nslow = nhead + (x.khi - x.ihi);
+    if (nslow && lane < (int)nslow) {
+        const uint32_t k = (uint32_t)lane < nhead ? x.klo + lane : x.ihi + (lane - nhead);
+        const uint64_t a = x.dst + 16u * k;
+        if (a + 16 > total) {  // the output's last, partial word: byte stores
+#pragma clang loop vectorize(disable) unroll(disable)
+            for (uint64_t p = a; p < total; ++p) {
+                const uint32_t b = (uint32_t)(p - a);
+                const uint32_t v = (b & 8u) ? ((b & 4u) ? R.sv.w : R.sv.z) : ((b & 4u) ? R.sv.y : R.sv.x);
+                dst[p] = (uint8_t)(v >> (8 * (b & 3u)));
+            }
+        }
+    }
+    u32x4 out[kUnitW];
+#pragma unroll
+    for (int i = 0; i < kUnitW; ++i) {
+        const uint32_t k = lane + 64 * i;
+        u32x4 v = R.lo[i];
+        if (x.fast && x.delta) {
+            u32x4 hi;
+            hi.x = __shfl_down(R.lo[i].x, 1, 64);
+            hi.y = __shfl_down(R.lo[i].y, 1, 64);
+            hi.z = __shfl_down(R.lo[i].z, 1, 64);
+            hi.w = __shfl_down(R.lo[i].w, 1, 64);
+            if (i + 1 < kUnitW) {  // word 64 (i + 1) for lane 63 (the unit's last word is never below last)
+                const u32x4 nx = readlane0(R.lo[i + 1 < kUnitW ? i + 1 : i]);
+                if (lane == 63) hi = nx;
+            }
+            if (k == x.last) hi = R.ex;
+            v = funnel16(R.lo[i], hi, x.delta);
+        }
+        out[i] = v ^ x.rk;
+        // composed words of this instruction's 64 (wave-uniform test)
+        const uint32_t c0 = 64u * i, c1 = c0 + 64u;
+        if ((x.klo < x.ilo && x.klo < c1 && x.ilo > c0) || (x.ihi < x.khi && x.ihi < c1 && x.khi > c0)) {
+            const bool slow = (k >= x.klo && k < x.ilo) || (k >= x.ihi && k < x.khi);
+            const int from = (int)(k < x.ilo ? k - x.klo : nhead + (k - x.ihi)) & 63;
+            const u32x4 w = shfl16(R.sv, from);
+            if (slow) out[i] = w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kUnitW; ++i) {
+        const uint32_t k = lane + 64 * i;
+        const uint64_t a = x.dst + 16u * k;
+        if (k >= x.klo && k < x.khi && a + 16 <= total)
+            __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + a));
+    }
+}
+
+// One wave per unit: kUnitW words per lane, 1 KiB per wave-instruction.
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                       const uint64_t* __restrict__ start,
@@ -595,90 +732,15 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     const uint64_t total = start[n];
     // no early exit between these loads and their uses (the compiler would sink
     // the record load below the count's wait): an out-of-range wave owns no words
-    const uint32_t khi = (u < total_units && st == 0) ? r.own >> 16 : 0u;
+    const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
     // keep every field's load above the exit (one wait for all of them)
     asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
-    if (khi == 0) return;  // wave-uniform, after the record's wait
-    const uint32_t klo = r.own & 0x1FFu, head_f = (r.own >> 12) & 0xFu;
-    const uint32_t ilo = r.inner & 0xFFFFu, ihi = r.inner >> 16;
-    const uint32_t delta = (uint32_t)(r.src & 15u);  // same for every word of the unit
-    const uint8_t* s0 = src + (r.src - delta);
-    constexpr int kW = kUnitWords / 64;
+    if (x.khi == 0) return;  // wave-uniform, after the record's wait
     // Every load is issued before the first store (vmcnt also counts stores, so
     // a load issued after a store would make its wait cover that store too).
-    // Fast-path addresses are clamped to [ilo, ihi - 1] instead of predicating.
-    const bool fast = ihi > ilo;
-    const uint32_t last = fast ? ihi - 1 : ilo;
-    u32x4 lo[kW], ex[kW];
-    if (!fast) {
-#pragma unroll
-        for (int i = 0; i < kW; ++i) lo[i] = u32x4{0, 0, 0, 0};
-    } else {
-#pragma unroll
-        for (int i = 0; i < kW; ++i) {
-            const uint32_t k = lane + 64 * i;
-            const uint32_t kk = k < ilo ? ilo : (k < last ? k : last);
-            lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * kk));
-        }
-        if (delta) {
-            // the next aligned source word comes from lane + 1, except on lane 63
-            // and on the last interior word, which load it themselves
-#pragma unroll
-            for (int i = 0; i < kW; ++i) {
-                const uint32_t k = lane + 64 * i;
-                if (lane == 63 || k >= last)
-                    ex[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * ((k < last ? k : last) + 1));
-            }
-        }
-    }
-    // Edge words (composed by unit_rec): [klo, ilo) then [ihi, khi), one per lane.
-    const uint32_t nhead = ilo - klo, nslow = nhead + (khi - ihi);
-    u32x4 sv = u32x4{0, 0, 0, 0};
-    if (nslow && lane < (int)nslow) {
-        const uint32_t q = (uint32_t)lane < nhead ? lane : head_f + (lane - nhead);
-        sv = edge[(uint64_t)r.f * kEdgeWords + q];
-        const uint32_t k = (uint32_t)lane < nhead ? klo + lane : ihi + (lane - nhead);
-        const uint64_t a = r.dst + 16u * k;
-        if (a + 16 > total) {  // the output's last, partial word: byte stores
-#pragma clang loop vectorize(disable) unroll(disable)
-            for (uint64_t p = a; p < total; ++p) {
-                const uint32_t b = (uint32_t)(p - a);
-                const uint32_t v = (b & 8u) ? ((b & 4u) ? sv.w : sv.z) : ((b & 4u) ? sv.y : sv.x);
-                dst[p] = (uint8_t)(v >> (8 * (b & 3u)));
-            }
-        }
-    }
-    u32x4 out[kW];
-#pragma unroll
-    for (int i = 0; i < kW; ++i) {
-        const uint32_t k = lane + 64 * i;
-        u32x4 v = lo[i];
-        if (fast && delta) {
-            u32x4 hi;
-            hi.x = __shfl_down(lo[i].x, 1, 64);
-            hi.y = __shfl_down(lo[i].y, 1, 64);
-            hi.z = __shfl_down(lo[i].z, 1, 64);
-            hi.w = __shfl_down(lo[i].w, 1, 64);
-            if (lane == 63 || k >= last) hi = ex[i];
-            v = funnel16(lo[i], hi, delta);
-        }
-        out[i] = v ^ r.rk;
-        // composed words of this instruction's 64 (wave-uniform test)
-        const uint32_t c0 = 64u * i, c1 = c0 + 64u;
-        if ((klo < ilo && klo < c1 && ilo > c0) || (ihi < khi && ihi < c1 && khi > c0)) {
-            const bool slow = (k >= klo && k < ilo) || (k >= ihi && k < khi);
-            const int from = (int)(k < ilo ? k - klo : nhead + (k - ihi)) & 63;
-            const u32x4 w = shfl16(sv, from);
-            if (slow) out[i] = w;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < kW; ++i) {
-        const uint32_t k = lane + 64 * i;
-        const uint64_t a = r.dst + 16u * k;
-        if (k >= klo && k < khi && a + 16 <= total)
-            __builtin_nontemporal_store(out[i], reinterpret_cast<u32x4*>(dst + a));
-    }
+    UnitRegs R;
+    unit_issue(x, lane, src, edge, R);
+    unit_finish(x, lane, dst, total, R);
 }
 
 // ------------------------------ header unpack / validate ------------------------------
@@ -771,11 +833,12 @@ struct CopyWs {
 };
 
 static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
-// sum of unit_bound(R_f) <= total / 4096 + 1.25 n (and total <= cap)
+// sum of unit_bound(R_f) <= total / (16 U) + n (1 + 63 / U) (and total <= cap)
 // (rounded up to whole blocks: every wave of the copy grid reads its record)
 static uint64_t max_units(uint32_t n, uint64_t cap)
 {
-    const uint64_t u = (cap + kUnitWords * 16 - 1) / (kUnitWords * 16) + 2ull * n;
+    // unit_bound(R) <= R / (16 U) + 1 + 63 / U per frame (U = kUnitWords)
+    const uint64_t u = (cap + kUnitWords * 16 - 1) / (kUnitWords * 16) + n + (63ull * n + kUnitWords - 1) / kUnitWords + 1;
     return (u + kBlock / 64 - 1) / (kBlock / 64) * (kBlock / 64);
 }
 static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }

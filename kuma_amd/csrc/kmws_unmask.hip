@@ -206,6 +206,47 @@ __global__ void __launch_bounds__(kBlock) unmask_persist_kernel(uint8_t* __restr
     }
 }
 
+// Grid-stride like unmask_persist_kernel, software-pipelined for real: two
+// register sets used in turn (a copy from one to the other waits for the loads
+// in flight), and a loop with one exit at the bottom -- both steps run every
+// trip, a step past the end loads a clamped tile and stores nothing -- so the
+// wait before a tile's stores counts only that tile's loads.
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_pipe_kernel(uint8_t* __restrict__ base,
+                                                             const kmws_desc* __restrict__ d, uint32_t n,
+                                                             const uint32_t* __restrict__ map,
+                                                             const WsHead* __restrict__ head, uint32_t nfull)
+{
+    using Cfg = UnmaskCfg<V>;
+    __shared__ uint64_t s_off[Cfg::kCap];
+    __shared__ uint64_t s_end[Cfg::kCap];
+    __shared__ uint32_t s_key[Cfg::kCap];
+    uint32_t t = blockIdx.x;
+    if (t >= nfull) return;
+    const bool ok = head->status == 0;
+    const uint32_t last = nfull - 1;
+    u32x4 va[V], vb[V];
+    load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, va);
+    auto step = [&](const u32x4(&vc)[V], u32x4(&vn)[V]) __attribute__((always_inline)) {
+        const uint32_t tn = t + gridDim.x;
+        const bool more = tn < nfull;
+        load_tile<V, true>(base, (uint64_t)(more ? tn : last) * Cfg::kTile, 0, vn);
+        __builtin_amdgcn_sched_barrier(0);
+        const bool live = t < nfull;
+        const uint32_t tt = live ? t : last;
+        const uint64_t lo = (uint64_t)tt * Cfg::kTile;
+        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[tt], ok && live, vc, s_off, s_end, s_key);
+        __builtin_amdgcn_sched_barrier(0);
+        t = tn;
+        return more;
+    };
+    for (;;) {
+        const bool a = step(va, vb);
+        const bool b = step(vb, va);
+        if (!(a & b)) break;
+    }
+}
+
 // ---- synthetic fill: byte i = byte (i & 7) of splitmix64(seed + (i >> 3)) ----
 __global__ void __launch_bounds__(kBlock) fill_synthetic_kernel(uint8_t* __restrict__ base, uint64_t bytes,
                                                                 uint64_t seed)
@@ -363,12 +404,46 @@ static kmws_status launch_apply_persist(uint8_t* base, uint64_t span, const kmws
 }
 
 template <int V>
+static kmws_status launch_apply_pipe(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                     const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t grid)
+{
+    using Cfg = UnmaskCfg<V>;
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    if (n == 0 || span == 0) return KMWS_OK;
+    const WsHead* head = static_cast<const WsHead*>(workspace);
+    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
+    const uint64_t nfull = span / Cfg::kTile;
+    if (nfull > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    if (nfull) {
+        const uint32_t g = (uint32_t)(nfull < grid ? nfull : grid);
+        hipLaunchKernelGGL(unmask_pipe_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
+                           (uint32_t)nfull);
+    }
+    if (ntiles > nfull)  // the partial last tile
+        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
+                           (uint32_t)nfull);
+    return hip_status(hipGetLastError());
+}
+
+template <int V>
 static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                  void* workspace, size_t ws_bytes, hipStream_t s)
 {
     kmws_status st = launch_plan<V>(span, descs, n, workspace, ws_bytes, s);
     if (st != KMWS_OK) return st;
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
+}
+
+// Schedule code: 0 = one block per tile; otherwise the grid size (a multiple of
+// 2), plus 1 for the software-pipelined grid (unmask_pipe_kernel).
+static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                   const void* workspace, size_t ws_bytes, hipStream_t s)
+{
+    if (code == 0) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
+    if (code & 1u) return launch_apply_pipe<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code & ~1u);
+    return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code);
 }
 
 static uint32_t current_schedule()
@@ -417,9 +492,7 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint32_t grid = current_schedule();
-    if (grid) return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s, grid);
-    return launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s);
+    return launch_schedule(current_schedule(), base, span, descs, n, workspace, workspace_bytes, s);
 }
 
 int kmws_unmask_schedule(void) { return (int)current_schedule(); }
@@ -436,7 +509,9 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     hipStream_t s = static_cast<hipStream_t>(stream);
     kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    static const uint32_t cand[] = {0u, 16384u, 32768u};
+    // one block per tile; persistent 16 K / 32 K blocks; pipelined 16 K / 64 K blocks
+    // (which of them wins differs from box to box: profiles/r01c_unmask_schedules.txt)
+    static const uint32_t cand[] = {0u, 16384u, 32768u, 16384u | 1u, 65536u | 1u};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {
@@ -449,8 +524,7 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
         for (uint32_t g : cand) {
             if (hipEventRecord(e0, s) != hipSuccess) { st = KMWS_ERR_FAILED; break; }
             for (int k = 0; k < 2 && st == KMWS_OK; ++k)
-                st = g ? launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s, g)
-                       : launch_apply<kUnmaskV>(base, span, descs, n, workspace, workspace_bytes, s);
+                st = launch_schedule(g, base, span, descs, n, workspace, workspace_bytes, s);
             if (st != KMWS_OK || hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
                 st = st != KMWS_OK ? st : KMWS_ERR_FAILED;
                 break;
@@ -499,6 +573,14 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         if (st != KMWS_OK) return st;
         return variant == 8 ? launch_apply<4, 6>(base, span, descs, n, workspace, workspace_bytes, s)
                             : launch_apply<4, 8>(base, span, descs, n, workspace, workspace_bytes, s);
+    }
+    case 10:
+    case 11:
+    case 12: {  // 16 KiB tiles, pipelined persistent grid: 16384 / 32768 / 65536 blocks
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        static const uint32_t grids[] = {16384u, 32768u, 65536u};
+        return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, grids[variant - 10]);
     }
     default: return KMWS_ERR_INVALID_PARAM;
     }

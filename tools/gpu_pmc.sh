@@ -17,4 +17,8 @@ pass tiles_write WRITE_SIZE "--no-autotune" &&
 python3 tools/pmc_traffic.py "$OUT/tiles_fetch" "$OUT/tiles_write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json" &&
 pass persist_fetch FETCH_SIZE "--variant 4" &&
 pass persist_write WRITE_SIZE "--variant 4" &&
-python3 tools/pmc_traffic.py "$OUT/persist_fetch" "$OUT/persist_write" unmask_persist_kernel 1048576 65536 "$OUT/traffic_persist.json"
+python3 tools/pmc_traffic.py "$OUT/persist_fetch" "$OUT/persist_write" unmask_persist_kernel 1048576 65536 "$OUT/traffic_persist.json" &&
+[ -n "$PMC_PIPE" ] || exit 0
+pass pipe_fetch FETCH_SIZE "--variant 10" &&
+pass pipe_write WRITE_SIZE "--variant 10" &&
+python3 tools/pmc_traffic.py "$OUT/pipe_fetch" "$OUT/pipe_write" unmask_pipe_kernel 1048576 65536 "$OUT/traffic_pipe.json"
