@@ -88,16 +88,20 @@ def _cpu_model() -> str:
 
 def schedule_kernel(schedule: int) -> str:
     """Kernel that carries the unmask for a kmws_unmask_schedule() code."""
-    if schedule == 0:
+    if schedule in (0, 2):
+        return "unmask_split_kernel"
+    if schedule == 1:
         return "unmask_tiles_kernel"
     return "unmask_pipe_kernel" if schedule & 1 else "unmask_persist_kernel"
 
 
 def schedule_name(schedule: int) -> str:
-    if schedule == 0:
-        return "one block per 16 KiB tile"
+    if schedule in (0, 2):
+        return f"one block per 16 KiB tile, tiles dealt over {8 if schedule == 0 else 2} parts of the span"
+    if schedule == 1:
+        return "one block per 16 KiB tile, in order"
     kind = "pipelined persistent grid" if schedule & 1 else "persistent grid-stride"
-    return f"{kind}, {schedule & ~1} blocks (autotuned)"
+    return f"{kind}, {schedule & ~1} blocks"
 
 
 def traffic_from_profile(frames: int, frame_len: int, kernel: str):
@@ -215,7 +219,8 @@ def main():
     value = shard.aggregate_rate([span * a.steps] * world, [elapsed] * world) / 2**30
     alg_bytes = n * (2 * L + DESC_BYTES)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profile(n, L, schedule_kernel(schedule))
+    kernel = schedule_kernel(schedule) if variant is None else f"kmws_unmask_batch_variant({variant})"
+    traffic = traffic_from_profile(n, L, kernel)
 
     out = None
     if rank == 0:
@@ -238,7 +243,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": schedule_kernel(schedule),
+                         "kernel": kernel,
                          "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /

@@ -185,17 +185,27 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * on this batch (the XOR applied twice leaves the payload unchanged), times
  * them with events on `stream` (synchronizes) and makes the fastest the
  * current device's schedule for kmws_unmask_apply / kmws_unmask_batch.
- * Returns the chosen schedule (0 = one block per tile; else the grid size,
- * plus 1 for the pipelined grid) or a negative status.  kmws_unmask_schedule() reports the current one. */
+ * Returns the chosen schedule or a negative status: one block per 16 KiB tile
+ * with the tiles dealt over 8 parts of the span (0, the default), in order (1)
+ * or over 2 parts (2); >= 64: a persistent grid of that many blocks (+1: the
+ * pipelined grid).  kmws_unmask_schedule() reports the current one. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
 int kmws_unmask_schedule(void);
+/* Tuning info: blocks of the persistent unmask kernel resident at once on the
+ * current device (CUs x blocks per CU), or 0 on failure. */
+int kmws_unmask_resident_blocks(void);
 
 /* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2);
  * 16 KiB tiles on a persistent grid-stride grid of 8 K (3), 16 K (4), 24 K (5),
  * 32 K (6) or 64 K (7) blocks; one block per tile with registers capped for 6 (8)
  * or 8 (9) waves per SIMD; pipelined persistent grid of 16 K (10), 32 K (11) or
- * 64 K (12) blocks. */
+ * 64 K (12) blocks; work queue (one resident grid taking chunks of 1 (13), 4 (14)
+ * or 16 (15) tiles; chunks of 4 on twice the resident grid (16)); pipelined grid
+ * of 1, 2, 4 or 8 x the resident blocks (17-20); one block per 16 KiB tile dealt
+ * over 2, 4, 8, 16 (21-24) or 3, 6, 12, 32 (30-33) parts of the span, or in runs
+ * of 16 .. 65536 tiles over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8 parts
+ * (34, 35); any value >= 64: a schedule code as kmws_unmask_schedule() returns. */
 kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       void* workspace, size_t workspace_bytes, void* stream, int variant);
 

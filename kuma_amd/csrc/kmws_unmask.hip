@@ -175,6 +175,43 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
     }
 }
 
+// One block per full tile like unmask_tiles_kernel, blocks dealt over `k`
+// equal parts of the span: block b takes tile (b mod k) * (nfull / k) + b / k,
+// so the blocks in flight stream k windows far apart instead of one (the
+// blocks past k * (nfull / k) take the remaining tiles in order).  With c > 0
+// the span is cut into runs of c tiles instead, dealt round-robin to the k
+// residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
+// its own runs).
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
+                                                              const kmws_desc* __restrict__ d, uint32_t n,
+                                                              const uint32_t* __restrict__ map,
+                                                              const WsHead* __restrict__ head, uint32_t nfull,
+                                                              uint32_t k, uint32_t c, uint32_t b0)
+{
+    using Cfg = UnmaskCfg<V>;
+    __shared__ uint64_t s_off[Cfg::kCap];
+    __shared__ uint64_t s_end[Cfg::kCap];
+    __shared__ uint32_t s_key[Cfg::kCap];
+    const uint32_t b = b0 + blockIdx.x;
+    uint32_t tile = b;
+    if (c == 0) {  // k equal parts
+        const uint32_t q = nfull / k;
+        if (b < q * k) tile = (b % k) * q + b / k;
+    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k
+        const uint64_t run = (uint64_t)k * c;
+        if (b < nfull / run * run) {
+            const uint32_t x = b % k, i = b / k;
+            tile = (i / c) * (uint32_t)run + x * c + i % c;
+        }
+    }
+    const uint64_t lo = (uint64_t)tile * Cfg::kTile;
+    u32x4 v[V];
+    load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[tile], head->status == 0, v, s_off, s_end, s_key);
+}
+
 // Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
 // and issues the next tile's loads before finishing the current one.
 template <int V>
@@ -244,6 +281,76 @@ __global__ void __launch_bounds__(kBlock) unmask_pipe_kernel(uint8_t* __restrict
         const bool a = step(va, vb);
         const bool b = step(vb, va);
         if (!(a & b)) break;
+    }
+}
+
+// Work queue over the full tiles: a grid of about one resident block per slot
+// takes chunks of `chunk` tiles from a counter in the workspace head (pad[0]),
+// so every block streams until the queue is empty and no block generation is
+// left half full at the end (the grid-stride schedules above run 16-32 block
+// generations; a grid that is not a multiple of the resident count leaves
+// the last one part-empty).  Thread 0 takes the NEXT chunk while the current
+// one streams (one device-scope atomic per chunk) and publishes it through LDS
+// at the chunk boundary.  The last block out resets the counters (pad[0..1]),
+// so the workspace is left as the plan wrote it.
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_queue_kernel(uint8_t* __restrict__ base,
+                                                              const kmws_desc* __restrict__ d, uint32_t n,
+                                                              const uint32_t* __restrict__ map,
+                                                              WsHead* __restrict__ head, uint32_t nfull,
+                                                              uint32_t chunk)
+{
+    using Cfg = UnmaskCfg<V>;
+    __shared__ uint64_t s_off[Cfg::kCap];
+    __shared__ uint64_t s_end[Cfg::kCap];
+    __shared__ uint32_t s_key[Cfg::kCap];
+    __shared__ uint32_t s_grab;
+    uint32_t* q = &head->pad[0];
+    const bool ok = head->status == 0;
+    const bool lead = threadIdx.x == 0;
+    if (lead) s_grab = atomicAdd(q, chunk);
+    __syncthreads();
+    uint32_t t = s_grab;
+    // Thread 0 takes the next chunk.  Every lane of wave 0 runs the atomic (the
+    // others add 0): a lane-0-only atomic ends a divergent branch, and the
+    // compiler waits for ALL outstanding loads at its join.
+    const bool w0 = threadIdx.x < 64;
+    const uint32_t add = lead ? chunk : 0u;
+    uint32_t next = w0 ? atomicAdd(q, add) : 0u;
+    if (t < nfull) {
+        uint32_t cend = t + chunk < nfull ? t + chunk : nfull;
+        u32x4 va[V], vb[V];
+        load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, va);
+        auto step = [&](const u32x4(&vc)[V], u32x4(&vn)[V]) __attribute__((always_inline)) {
+            uint32_t tn = t + 1;
+            if (tn >= cend) {  // block-uniform: chunk boundary
+                __syncthreads();  // every lane has read the previous s_grab
+                if (lead) s_grab = next;
+                __syncthreads();
+                tn = s_grab;
+                cend = tn + chunk < nfull ? tn + chunk : nfull;
+                if (w0) next = atomicAdd(q, tn < nfull ? add : 0u);
+            }
+            const bool more = tn < nfull;
+            load_tile<V, true>(base, (uint64_t)(more ? tn : t) * Cfg::kTile, 0, vn);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t lo = (uint64_t)t * Cfg::kTile;
+            finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[t], ok, vc, s_off, s_end, s_key);
+            __builtin_amdgcn_sched_barrier(0);
+            t = tn;
+            return more;
+        };
+        for (;;) {
+            if (!step(va, vb)) break;
+            if (!step(vb, va)) break;
+        }
+    }
+    if (lead) {
+        __threadfence();
+        if (atomicAdd(&head->pad[1], 1u) == gridDim.x - 1) {  // every block is past its last take
+            atomicExch(&head->pad[0], 0u);
+            atomicExch(&head->pad[1], 0u);
+        }
     }
 }
 
@@ -319,10 +426,11 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
 // Tile geometry used by the product path (tuned on MI355X).
 constexpr int kUnmaskV = 4;
 
-// Apply schedule per device: 0 = one block per 16 KiB tile (default: 74.5-75 %
-// of HBM peak on every box measured), or a persistent grid-stride grid of that
-// many blocks (+1.5-3 % on most boxes, -12 % on some; profiles/r01_unmask_
-// variants_5boxes.txt).  Set only by kmws_unmask_autotune.
+// Apply schedule per device (codes: launch_schedule).  Default 0: one block per
+// 16 KiB tile, consecutive blocks dealt over 8 parts of the span, so the blocks
+// in flight stream 8 windows far apart: 82-83 % of HBM peak where the in-order
+// grid gets 74.5-75 % (profiles/r01c_unmask_schedules.txt).  Set only by
+// kmws_unmask_autotune.
 constexpr int kMaxDevices = 64;
 static uint32_t g_schedule[kMaxDevices];
 using ProdCfg = UnmaskCfg<kUnmaskV>;
@@ -427,6 +535,72 @@ static kmws_status launch_apply_pipe(uint8_t* base, uint64_t span, const kmws_de
     return hip_status(hipGetLastError());
 }
 
+// Resident blocks of a kernel on the current device (CUs x blocks per CU).
+static uint32_t resident_blocks(const void* kernel)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) return 0;
+    return (uint32_t)(cus * per);
+}
+
+template <int V>
+static kmws_status launch_apply_queue(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                      const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t per_slot,
+                                      uint32_t chunk)
+{
+    using Cfg = UnmaskCfg<V>;
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    if (n == 0 || span == 0) return KMWS_OK;
+    // the kernel only borrows the head's queue words and zeroes them again
+    WsHead* head = const_cast<WsHead*>(static_cast<const WsHead*>(workspace));
+    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
+    const uint64_t nfull = span / Cfg::kTile;
+    if (nfull > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    if (nfull) {
+        const uint32_t r = resident_blocks(reinterpret_cast<const void*>(unmask_queue_kernel<V>));
+        if (r == 0) return KMWS_ERR_FAILED;
+        const uint64_t want = (uint64_t)r * per_slot;
+        const uint32_t g = (uint32_t)(want < nfull ? want : nfull);
+        hipLaunchKernelGGL(unmask_queue_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
+                           (uint32_t)nfull, chunk);
+    }
+    if (ntiles > nfull)  // the partial last tile
+        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
+                           (uint32_t)nfull);
+    return hip_status(hipGetLastError());
+}
+
+template <int V>
+static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                      const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
+                                      uint32_t c = 0)
+{
+    using Cfg = UnmaskCfg<V>;
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    if (n == 0 || span == 0) return KMWS_OK;
+    const WsHead* head = static_cast<const WsHead*>(workspace);
+    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
+    const uint64_t nfull = span / Cfg::kTile;
+    if (nfull > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    // a launch may hold at most 2^32 work-items: huge spans go in pieces of blocks
+    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
+    for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
+        const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
+        hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
+                           head, (uint32_t)nfull, k, c, (uint32_t)b0);
+    }
+    if (ntiles > nfull)  // the partial last tile
+        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
+                           (uint32_t)nfull);
+    return hip_status(hipGetLastError());
+}
+
 template <int V>
 static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                  void* workspace, size_t ws_bytes, hipStream_t s)
@@ -436,12 +610,17 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
 }
 
-// Schedule code: 0 = one block per tile; otherwise the grid size (a multiple of
-// 2), plus 1 for the software-pipelined grid (unmask_pipe_kernel).
+// Schedule code: one block per tile with the tiles dealt over 8 parts of the
+// span (0, the default), in order (1), or over 2 parts (2); codes >= 64: a
+// persistent grid of that many blocks, grid-stride (even) or software-pipelined
+// (odd, grid = code - 1).
 static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                    const void* workspace, size_t ws_bytes, hipStream_t s)
 {
-    if (code == 0) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
+    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
+    if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
+    if (code == 2) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 2u);
+    if (code < 64) return KMWS_ERR_INVALID_PARAM;
     if (code & 1u) return launch_apply_pipe<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code & ~1u);
     return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code);
 }
@@ -497,6 +676,11 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
 
 int kmws_unmask_schedule(void) { return (int)current_schedule(); }
 
+int kmws_unmask_resident_blocks(void)
+{
+    return (int)resident_blocks(reinterpret_cast<const void*>(kmws::unmask_pipe_kernel<kUnmaskV>));
+}
+
 // Times each schedule on the caller's batch, twice per schedule (XOR applied
 // twice is the identity, so the payload is unchanged on return), and keeps the
 // fastest as this device's kmws_unmask_apply schedule.  Synchronizes.
@@ -509,9 +693,9 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     hipStream_t s = static_cast<hipStream_t>(stream);
     kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    // one block per tile; persistent 16 K / 32 K blocks; pipelined 16 K / 64 K blocks
-    // (which of them wins differs from box to box: profiles/r01c_unmask_schedules.txt)
-    static const uint32_t cand[] = {0u, 16384u, 32768u, 16384u | 1u, 65536u | 1u};
+    // one block per tile dealt over 8 / 2 parts, in order; persistent 2 M blocks
+    // (2 tiles each); pipelined 64 K blocks (profiles/r01c_unmask_schedules.txt)
+    static const uint32_t cand[] = {0u, 2u, 1u, 2097152u, 65536u | 1u};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {
@@ -582,7 +766,66 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         static const uint32_t grids[] = {16384u, 32768u, 65536u};
         return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, grids[variant - 10]);
     }
-    default: return KMWS_ERR_INVALID_PARAM;
+    case 13:
+    case 14:
+    case 15:
+    case 16: {  // 16 KiB tiles, work queue: chunk 1 / 4 / 16 tiles on the resident grid, chunk 4 on twice it
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        static const uint32_t chunks[] = {1u, 4u, 16u, 4u};
+        return launch_apply_queue<4>(base, span, descs, n, workspace, workspace_bytes, s, variant == 16 ? 2u : 1u,
+                                     chunks[variant - 13]);
+    }
+    case 17:
+    case 18:
+    case 19:
+    case 20: {  // 16 KiB tiles, pipelined grid of 1 / 2 / 4 / 8 x the resident blocks
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        const uint32_t r = resident_blocks(reinterpret_cast<const void*>(unmask_pipe_kernel<4>));
+        if (r == 0) return KMWS_ERR_FAILED;
+        return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, r << (variant - 17));
+    }
+    case 21:
+    case 22:
+    case 23:
+    case 24: {  // 16 KiB tiles, one block per tile, blocks dealt over 2 / 4 / 8 / 16 parts of the span
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 2u << (variant - 21));
+    }
+    case 25:
+    case 26:
+    case 27:
+    case 28:
+    case 29: {  // 16 KiB tiles, one block per tile, runs of 16 / 128 / 1024 / 8192 / 65536 tiles per XCD residue
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u,
+                                     16u << (3 * (variant - 25)));
+    }
+    case 30:
+    case 31:
+    case 32:
+    case 33: {  // 16 KiB tiles, one block per tile, blocks dealt over 3 / 6 / 12 / 32 parts of the span
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        static const uint32_t ks[] = {3u, 6u, 12u, 32u};
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, ks[variant - 30]);
+    }
+    case 34:
+    case 35: {  // 32 KiB tiles, one block per tile, blocks dealt over 2 / 8 parts of the span
+        kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, variant == 34 ? 2u : 8u);
+    }
+    default:
+        if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)
+            kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+            if (st != KMWS_OK) return st;
+            return launch_schedule((uint32_t)variant, base, span, descs, n, workspace, workspace_bytes, s);
+        }
+        return KMWS_ERR_INVALID_PARAM;
     }
 }
 

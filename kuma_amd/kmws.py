@@ -31,7 +31,7 @@ EXPORTS = [
     "kmws_encode_header", "kmws_header_size", "kmws_decoder_create", "kmws_decoder_destroy",
     "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
     "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
-    "kmws_unmask_batch_variant", "kmws_unmask_autotune", "kmws_unmask_schedule", "kmws_read_status", "kmws_fill_synthetic",
+    "kmws_unmask_batch_variant", "kmws_unmask_autotune", "kmws_unmask_schedule", "kmws_unmask_resident_blocks", "kmws_read_status", "kmws_fill_synthetic",
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
         "kmws_unmask_apply": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_autotune": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_schedule": (i32, []),
+        "kmws_unmask_resident_blocks": (i32, []),
         "kmws_unmask_batch_variant": (i32, [u8p, u64, vp, u32, vp, sz, vp, i32]),
         "kmws_read_status": (i32, [vp, C.POINTER(C.c_uint32), vp]),
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
@@ -362,6 +363,10 @@ def unmask_autotune(base, descs, ws: Workspace, span: Optional[int] = None, stre
 
 def unmask_schedule() -> int:
     return lib().kmws_unmask_schedule()
+
+
+def unmask_resident_blocks() -> int:
+    return lib().kmws_unmask_resident_blocks()
 
 
 def unmask_plan(descs, ws: Workspace, span: int, stream=None) -> None:

@@ -93,7 +93,7 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 65537])
 def test_unmask_parity(torch_dev, kind, variant):
     rng = np.random.default_rng(abs(hash((kind, variant))) % 2**32)
     buf, descs = layout(kind, rng)
@@ -197,9 +197,39 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
     ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
-    assert choice in (0, 16384, 32768, 16385, 65537) and kmws.unmask_schedule() == choice
+    assert choice in (0, 2, 1, 2097152, 65537) and kmws.unmask_schedule() == choice
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
     got, st = run_gpu(torch, buf, descs)
     assert st == 0 and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("frame_len", [65536, 65531, 3000])
+@pytest.mark.parametrize("variant", [None, 4, 10, 13, 14, 15, 16, 17, 20, 21, 24, 25, 27, 2097152])
+def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len):
+    """512 MiB arena (32 K tiles: several tiles and queue chunks per block of the
+    persistent / queue schedules), payload generated on the device, every byte
+    checked on the device against the generator (payload ^ key inside frames,
+    untouched gaps).  Applied twice more on the same plan (XOR twice = identity)
+    with the queue schedules, whose counters must be back at zero."""
+    torch = torch_dev
+    from kuma_amd import kmws
+    stride, span = 65536 if frame_len > 4096 else 4096, 512 << 20
+    n = span // stride
+    base = torch.empty(span, dtype=torch.uint8, device="cuda")
+    descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    kmws.fill_synthetic(base, 1234)
+    kmws.fill_uniform_descs(descs, stride, frame_len, 99)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span))
+    for _ in range(3):
+        kmws.unmask_batch(base, descs, ws, span, variant=variant)
+    torch.cuda.synchronize()
+    assert ws.status() == 0
+    assert kmws.check_unmasked(base, 1234, descs) == 0
+
+
+def test_resident_blocks_reported(torch_dev):
+    from kuma_amd import kmws
+    r = kmws.unmask_resident_blocks()
+    assert r > 0 and r % torch_dev.cuda.get_device_properties(0).multi_processor_count == 0

@@ -12,8 +12,11 @@ pass() {  # name counter bench-args
   timeout -k 10 300 rocprofv3 --pmc "$2" --kernel-trace --output-format csv -d "$PWD/$OUT/$1" -o run -- \
     python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-verify $3 > "$OUT/$1.json" 2> "$OUT/$1.err"
 }
-pass tiles_fetch FETCH_SIZE "--no-autotune" &&
-pass tiles_write WRITE_SIZE "--no-autotune" &&
+pass split_fetch FETCH_SIZE "--no-autotune" &&
+pass split_write WRITE_SIZE "--no-autotune" &&
+python3 tools/pmc_traffic.py "$OUT/split_fetch" "$OUT/split_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split.json" &&
+pass tiles_fetch FETCH_SIZE "--variant 0" &&
+pass tiles_write WRITE_SIZE "--variant 0" &&
 python3 tools/pmc_traffic.py "$OUT/tiles_fetch" "$OUT/tiles_write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json" &&
 pass persist_fetch FETCH_SIZE "--variant 4" &&
 pass persist_write WRITE_SIZE "--variant 4" &&
