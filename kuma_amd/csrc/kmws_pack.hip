@@ -84,6 +84,10 @@ __device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b +
 // lane measured the same or slower on cfg3/cfg4/64 KiB frames (within the
 // +-4 % run-to-run spread of one box; tools/gpu_ab_units.sh).
 constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
+#ifndef KMWS_COPY_SPLIT_DEFAULT
+#define KMWS_COPY_SPLIT_DEFAULT 8
+#endif
+constexpr uint32_t kCopySplit = KMWS_COPY_SPLIT_DEFAULT;
 constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
 #ifndef KMWS_LINE_BYTES
 #define KMWS_LINE_BYTES 64
@@ -718,12 +722,17 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ ubase,
                                                       const UnitRec* __restrict__ rec,
                                                       const u32x4* __restrict__ edge,
-                                                      const WsHead* __restrict__ head, uint64_t unit_base)
+                                                      const WsHead* __restrict__ head, uint64_t unit_base,
+                                                      uint32_t split)
 {
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: provably uniform, so the record is one scalar load
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t u = unit_base + (uint64_t)blockIdx.x * (kBlock / 64) + wave;
+    // consecutive blocks dealt over `split` parts of the unit slots, so the
+    // blocks in flight stream that many windows of the output far apart
+    const uint32_t q = gridDim.x / split;
+    const uint32_t b = blockIdx.x < q * split ? (blockIdx.x % split) * q + blockIdx.x / split : blockIdx.x;
+    const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
     // record, slot count, status and total are independent scalar loads (one
     // latency level); slots past the count lie inside the workspace and are ignored
     const UnitRec r = rec[u];
@@ -902,13 +911,21 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
         return e ? atoi(e) : -1;
     }();
     const unsigned lds_pad = lds_env >= 0 ? (unsigned)lds_env : (cap / n >= 16384 ? 32768u : 0u);
+    // Blocks dealt over kCopySplit far-apart parts of the output (as the unmask
+    // schedule); KMWS_COPY_SPLIT overrides it (tuning).
+    static const uint32_t split = [] {
+        const char* e = getenv("KMWS_COPY_SPLIT");
+        const int v = e ? atoi(e) : -1;
+        return v >= 1 ? (uint32_t)v : kCopySplit;
+    }();
     const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
     constexpr uint64_t kWavesPerBlock = kBlock / 64;
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
     for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
         const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
         hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0);
+                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0,
+                           split);
     }
     return hip_status(hipGetLastError());
 }
