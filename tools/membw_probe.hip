@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <string>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -131,6 +132,58 @@ __global__ void __launch_bounds__(B) copy_tiles(const u32x4* a, u32x4* b)
     for (int i = 0; i < V; ++i) b[base + (uint64_t)B * i] = v[i];
 }
 
+// one block per tile, tiles dealt over K parts of the buffer (the product's split schedule)
+template <int V, int B, int K>
+__global__ void __launch_bounds__(B) xor_split_nt(u32x4* p, uint32_t c)
+{
+    const uint64_t q = gridDim.x / K;
+    const uint64_t t = K > 1 ? (blockIdx.x % K) * q + blockIdx.x / K : blockIdx.x;
+    const uint64_t base = t * B * V + threadIdx.x;
+    u32x4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = __builtin_nontemporal_load(p + base + (uint64_t)B * i);
+#pragma unroll
+    for (int i = 0; i < V; ++i) __builtin_nontemporal_store(v[i] ^ c, p + base + (uint64_t)B * i);
+}
+
+// read-only ceiling: XOR-reduce a tile, one word per block out (negligible writes)
+template <int V, int B, int K>
+__global__ void __launch_bounds__(B) read_split_nt(const u32x4* p, u32x4* out)
+{
+    const uint64_t q = gridDim.x / K;
+    const uint64_t t = K > 1 ? (blockIdx.x % K) * q + blockIdx.x / K : blockIdx.x;
+    const uint64_t base = t * B * V + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc ^= __builtin_nontemporal_load(p + base + (uint64_t)B * i);
+    if ((acc.x | acc.y | acc.z | acc.w) == 0x9e3779b9u) out[blockIdx.x] = acc;  // practically never
+}
+
+// write-only ceiling
+template <int V, int B, int K>
+__global__ void __launch_bounds__(B) write_split_nt(u32x4* p, uint32_t c)
+{
+    const uint64_t q = gridDim.x / K;
+    const uint64_t t = K > 1 ? (blockIdx.x % K) * q + blockIdx.x / K : blockIdx.x;
+    const uint64_t base = t * B * V + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < V; ++i) __builtin_nontemporal_store(u32x4{c, c, c, (uint32_t)i}, p + base + (uint64_t)B * i);
+}
+
+// copy half -> half with the split mapping
+template <int V, int B, int K>
+__global__ void __launch_bounds__(B) copy_split_nt(const u32x4* a, u32x4* b)
+{
+    const uint64_t q = gridDim.x / K;
+    const uint64_t t = K > 1 ? (blockIdx.x % K) * q + blockIdx.x / K : blockIdx.x;
+    const uint64_t base = t * B * V + threadIdx.x;
+    u32x4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = __builtin_nontemporal_load(a + base + (uint64_t)B * i);
+#pragma unroll
+    for (int i = 0; i < V; ++i) __builtin_nontemporal_store(v[i], b + base + (uint64_t)B * i);
+}
+
 __global__ void __launch_bounds__(256) fill_kernel(u32x4* p, uint64_t nw)
 {
     for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * 256)
@@ -144,7 +197,10 @@ int main(int argc, char** argv)
     uint8_t* buf = nullptr;
     CK(hipMalloc(&buf, bytes));
     const uint64_t nw = bytes / 16;
-    hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (u32x4*)buf, nw);
+    // argv[4] == "rand": splitmix64 payload (as bench.py) instead of the low-entropy counter pattern
+    const bool rand_fill = argc > 4 && std::string(argv[4]) == "rand";
+    if (rand_fill) kmws_fill_synthetic(buf, bytes, 12345, 0);
+    else hipLaunchKernelGGL(fill_kernel, dim3(8192), dim3(256), 0, 0, (u32x4*)buf, nw);
     // product path inputs: 64 KiB frames over the same buffer
     const uint32_t nf = (uint32_t)(bytes / 65536);
     kmws_desc* d = nullptr;
@@ -170,12 +226,21 @@ int main(int argc, char** argv)
         {"product variant 6 (persistent x32768)", 27}, {"product variant 7 (persistent x65536)", 28},
         {"product variant 8 (>=6 waves/SIMD)", 29}, {"product variant 9 (>=8 waves/SIMD)", 30},
     };
-    if (argc > 3) {  // "product": only the product variants, interleaved
+    const bool ceil_mode = argc > 3 && std::string(argv[3]) == "ceil";
+    if (ceil_mode) {  // read-only / write-only / copy / in-place ceilings, in order vs split
+        vars = {{"read-only nt V4, in order", 40}, {"read-only nt V4, split 8", 41},
+                {"write-only nt V4, in order", 42}, {"write-only nt V4, split 8", 43},
+                {"copy nt V4 (half -> half), in order", 44}, {"copy nt V4 (half -> half), split 8", 45},
+                {"xor nt V4, in order", 46}, {"xor nt V4, split 2", 47}, {"xor nt V4, split 8", 48},
+                {"product kmws_unmask_apply (default schedule)", 9}};
+    } else if (argc > 3) {  // "product": only the product variants, interleaved
         std::vector<Var> keep;
         for (auto& v : vars)
             if (v.kind == 9 || v.kind == 11 || v.kind >= 23) keep.push_back(v);
         vars = keep;
     }
+    u32x4* sink = nullptr;
+    CK(hipMalloc(&sink, (nw / 1024) * sizeof(u32x4)));
     std::vector<std::vector<float>> ms(vars.size());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -214,6 +279,17 @@ int main(int argc, char** argv)
             case 28: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 7); break;
             case 29: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 8); break;
             case 30: kmws_unmask_batch_variant(buf, bytes, d, nf, ws, wsb, 0, 9); break;
+            case 40: hipLaunchKernelGGL((read_split_nt<4, 256, 1>), dim3(nw / 1024), dim3(256), 0, 0, (const u32x4*)buf, sink); break;
+            case 41: hipLaunchKernelGGL((read_split_nt<4, 256, 8>), dim3(nw / 1024), dim3(256), 0, 0, (const u32x4*)buf, sink); break;
+            case 42: hipLaunchKernelGGL((write_split_nt<4, 256, 1>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 43: hipLaunchKernelGGL((write_split_nt<4, 256, 8>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 44: hipLaunchKernelGGL((copy_split_nt<4, 256, 1>), dim3(nw / 2 / 1024), dim3(256), 0, 0,
+                                        (const u32x4*)buf, (u32x4*)(buf + bytes / 2)); break;
+            case 45: hipLaunchKernelGGL((copy_split_nt<4, 256, 8>), dim3(nw / 2 / 1024), dim3(256), 0, 0,
+                                        (const u32x4*)buf, (u32x4*)(buf + bytes / 2)); break;
+            case 46: hipLaunchKernelGGL((xor_split_nt<4, 256, 1>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 47: hipLaunchKernelGGL((xor_split_nt<4, 256, 2>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 48: hipLaunchKernelGGL((xor_split_nt<4, 256, 8>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
@@ -222,12 +298,15 @@ int main(int argc, char** argv)
             if (r > 0) ms[k].push_back(t);
         }
     }
-    printf("buffer %.1f GiB, %d reps (GB/s = 2 x bytes / time; copy moves half the buffer)\n",
+    printf("fill: %s\n", rand_fill ? "splitmix64 random" : "counter pattern {w, 1, 2, 3}");
+    printf("buffer %.1f GiB, %d reps (GB/s = bytes moved / time: 2 x buffer for in-place, 1 x for read-only,\n"
+           "write-only and copy (half -> half))\n",
            bytes / 1073741824.0, reps);
     for (size_t k = 0; k < vars.size(); ++k) {
         std::vector<float> v = ms[k];
         std::sort(v.begin(), v.end());
-        const double moved = vars[k].kind == 0 ? (double)bytes : 2.0 * bytes;
+        const int kd = vars[k].kind;
+        const double moved = (kd == 0 || kd == 44 || kd == 45 || (kd >= 40 && kd <= 43)) ? (double)bytes : 2.0 * bytes;
         printf("%-42s median %8.3f ms  best %8.3f ms  -> %7.0f GB/s (%.1f%% of 8 TB/s)\n", vars[k].name,
                v[v.size() / 2], v[0], moved / (v[v.size() / 2] * 1e-3) / 1e9,
                100.0 * moved / (v[v.size() / 2] * 1e-3) / 8e12);
