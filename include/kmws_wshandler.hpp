@@ -1,0 +1,251 @@
+// kmws_wshandler.hpp -- C++ drop-in for kuma's WSHandler over the kmws C ABI.
+//
+// Reference interface: kuma::ws::WSHandler (src/ws/WSHandler.h:32-91), the
+// codec member of WebSocket::Impl (src/ws/WebSocketImpl.h:140).  This header
+// gives the same class shape -- setMode/getMode, handleData, setFrameCallback,
+// reset, the static encodeFrameHeader / handleDataMask (x2) / isControlFrame --
+// on top of include/kmws_gpu.h, so WebSocket::Impl can hold either type.
+//
+// The class is a template over the caller's own types, so kuma instantiates it
+// with ITS FrameHeader, KMBuffer, WSError, WSMode and KMError
+// (INTEGRATION.md sec.3):
+//
+//   using KmwsHandler = kmws::BasicWSHandler<FrameHeader, KMBuffer, WSError, WSMode, KMError>;
+//
+// Requirements on the types (all met by kuma's):
+//   FrameHeader  fields fin rsv1 rsv2 rsv3 opcode mask plen (bitfields or
+//                integers), xpl.xpl64, maskey[4], length  (wsdefs.h:74-88)
+//   Buffer       Buffer(void* data, size_t capacity, size_t size) makes a
+//                non-owning view (kmbuffer.h:229-233, WSHandler.cpp:285);
+//                begin()/end() iterate the chain, it->readPtr(), it->length()
+//                (kmbuffer.h:706-772)
+//   WSError      enum with the values of wsdefs.h:56-67 (NOERR = 0 ...)
+//   WSMode       enum with CLIENT and SERVER (wsdefs.h:69-72)
+//   CbResult     whatever the frame callback returns (kuma: KMError); ignored,
+//                as WSHandler::handleFrame ignores it (WSHandler.cpp:286)
+//
+// kmws::ws below provides standalone types with those shapes, used by the
+// tests and by programs without kuma.
+//
+// Behaviour differences from the reference, all observable-byte-neutral:
+//  * payload unmasking runs on the GPU.  There is no CPU fallback: without a
+//    gfx950 device a masked frame makes handleData return INVALID_STATE and
+//    lastStatus() the kmws_status (KMWS_ERR_NOT_SUPPORTED); handleDataMask
+//    returns that status instead of void (callers that ignore the result, as
+//    kuma's do, compile unchanged).
+//  * self-destruction from inside the frame callback (the reference's
+//    DestroyDetector, WSHandler.cpp:284-287) is supported: the decoder state
+//    is reference-counted and outlives the feed that is delivering.
+#ifndef KMWS_WSHANDLER_HPP
+#define KMWS_WSHANDLER_HPP
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "kmws_gpu.h"
+
+namespace kmws {
+
+template <class FrameHeader, class Buffer, class WSError, class WSMode, class CbResult>
+class BasicWSHandler {
+public:
+    using FrameCallback = std::function<CbResult(FrameHeader, Buffer&)>;  // WSHandler.h:35
+
+    explicit BasicWSHandler(int device = 0) : st_(std::make_shared<State>(device)) {}
+    ~BasicWSHandler()
+    {
+        if (st_) st_->alive = false;  // a feed in progress keeps the state until it returns
+    }
+    BasicWSHandler(const BasicWSHandler&) = delete;
+    BasicWSHandler& operator=(const BasicWSHandler&) = delete;
+
+    // false if the decoder could not be created (bad device index)
+    bool valid() const { return st_->dec != nullptr; }
+
+    void setMode(WSMode mode)  // WSHandler.h:40
+    {
+        st_->mode = mode;
+        if (st_->dec) kmws_decoder_set_mode(st_->dec, mode == WSMode::SERVER ? KMWS_MODE_SERVER : KMWS_MODE_CLIENT);
+    }
+    WSMode getMode() const { return st_->mode; }  // WSHandler.h:41
+
+    // WSHandler::handleData (WSHandler.cpp:41-44): same return values and
+    // callback sequence; masked payloads lying wholly in `data` are unmasked
+    // there, in place.
+    WSError handleData(uint8_t* data, size_t len)
+    {
+        std::shared_ptr<State> keep = st_;
+        if (!keep->dec) return WSError::INVALID_STATE;
+        const int r = kmws_decoder_feed(keep->dec, data, len, &State::on_frame, keep.get());
+        if (!keep->alive) return WSError::DESTROYED;
+        keep->last_status = r < 0 ? r : KMWS_OK;
+        if (r < 0) return WSError::INVALID_STATE;  // device step failed: lastStatus() says why
+        return static_cast<WSError>(r);
+    }
+
+    // kmws_status of the last handleData: KMWS_OK, or why the GPU step failed
+    int lastStatus() const { return st_->last_status; }
+
+    void setFrameCallback(FrameCallback cb) { st_->cb = std::move(cb); }  // WSHandler.h:46
+
+    void reset()  // WSHandler.cpp:324-327
+    {
+        if (st_->dec) kmws_decoder_reset(st_->dec);
+    }
+
+    // WSHandler::encodeFrameHeader (WSHandler.cpp:46-106): 2/4/10 (+4) bytes
+    static int encodeFrameHeader(FrameHeader hdr, uint8_t hdr_buf[KMWS_MAX_HEADER_SIZE])
+    {
+        kmws_frame_hdr k;
+        std::memset(&k, 0, sizeof(k));
+        k.fin = hdr.fin;
+        k.rsv1 = hdr.rsv1;
+        k.rsv2 = hdr.rsv2;
+        k.rsv3 = hdr.rsv3;
+        k.opcode = hdr.opcode;
+        k.mask = hdr.mask;
+        k.plen = hdr.plen;
+        k.length = hdr.length;
+        std::memcpy(k.maskey, hdr.maskey, KMWS_MASK_KEY_SIZE);
+        return kmws_encode_header(&k, hdr_buf);
+    }
+
+    // WSHandler::handleDataMask(key, data, len) (WSHandler.cpp:303-310), on the GPU
+    static kmws_status handleDataMask(const uint8_t mask_key[KMWS_MASK_KEY_SIZE], uint8_t* data, size_t len,
+                                      int device = 0)
+    {
+        if (data == nullptr || len == 0) return KMWS_OK;  // :305
+        uint8_t* segs[1] = {data};
+        const size_t lens[1] = {len};
+        return kmws_mask_host_chain(mask_key, segs, lens, 1, device);
+    }
+
+    // WSHandler::handleDataMask(key, KMBuffer&) (WSHandler.cpp:312-322): the key
+    // phase continues across the chain's segments; on the GPU, one launch
+    static kmws_status handleDataMask(const uint8_t mask_key[KMWS_MASK_KEY_SIZE], Buffer& buf, int device = 0)
+    {
+        std::vector<uint8_t*> segs;
+        std::vector<size_t> lens;
+        for (auto it = buf.begin(); it != buf.end(); ++it) {
+            segs.push_back(static_cast<uint8_t*>(it->readPtr()));
+            lens.push_back(it->length());
+        }
+        if (segs.empty()) return KMWS_OK;
+        return kmws_mask_host_chain(mask_key, segs.data(), lens.data(), segs.size(), device);
+    }
+
+    static bool isControlFrame(uint8_t opcode) { return opcode >= 8; }  // WSHandler.h:52-54
+
+private:
+    struct State {
+        explicit State(int device) : dec(kmws_decoder_create(KMWS_MODE_CLIENT, device)) {}
+        ~State()
+        {
+            if (dec) kmws_decoder_destroy(dec);
+        }
+        State(const State&) = delete;
+        State& operator=(const State&) = delete;
+
+        // WSHandler::handleFrame (WSHandler.cpp:282-289): FrameHeader by value, a
+        // non-owning view of the payload, "destroyed" if the callback deleted
+        // the handler
+        static int on_frame(const kmws_frame_hdr* k, uint8_t* payload, size_t len, void* user)
+        {
+            State* s = static_cast<State*>(user);
+            FrameHeader h;
+            std::memset(static_cast<void*>(&h), 0, sizeof(h));
+            h.fin = k->fin;
+            h.rsv1 = k->rsv1;
+            h.rsv2 = k->rsv2;
+            h.rsv3 = k->rsv3;
+            h.opcode = k->opcode;
+            h.mask = k->mask;
+            h.plen = k->plen;
+            h.xpl.xpl64 = k->xpl64;
+            std::memcpy(h.maskey, k->maskey, KMWS_MASK_KEY_SIZE);
+            h.length = k->length;
+            Buffer view(static_cast<void*>(payload), len, len);
+            if (s->cb) {
+                FrameCallback cb = s->cb;  // the callback may replace or drop itself
+                (void)cb(h, view);
+            }
+            return s->alive ? 0 : 1;
+        }
+
+        kmws_decoder* dec;
+        FrameCallback cb;
+        WSMode mode = WSMode::CLIENT;
+        bool alive = true;
+        int last_status = KMWS_OK;
+    };
+    std::shared_ptr<State> st_;
+};
+
+// Standalone types with the reference's shapes, for programs without kuma.
+namespace ws {
+
+enum class WSError : int {  // wsdefs.h:56-67
+    NOERR = 0, NEED_MORE_DATA = 1, HANDSHAKE = 2, INVALID_PARAM = 3, INVALID_STATE = 4,
+    INVALID_FRAME = 5, INVALID_LENGTH = 6, PROTOCOL_ERROR = 7, CLOSED = 8, DESTROYED = 9
+};
+
+enum class WSMode { CLIENT, SERVER };  // wsdefs.h:69-72
+
+struct FrameHeader {  // wsdefs.h:74-88
+    uint8_t fin : 1;
+    uint8_t rsv1 : 1;
+    uint8_t rsv2 : 1;
+    uint8_t rsv3 : 1;
+    uint8_t opcode : 4;
+    uint8_t mask : 1;
+    uint8_t plen : 7;
+    union {
+        uint16_t xpl16;
+        uint64_t xpl64;
+    } xpl;
+    uint8_t maskey[KMWS_MASK_KEY_SIZE];
+    uint32_t length = 0;
+};
+
+// A non-owning segment chain with KMBuffer's view constructor and iteration
+// surface (kmbuffer.h:229-233, 706-772).
+class BufferChain {
+public:
+    struct Segment {
+        void* ptr;
+        size_t len;
+        void* readPtr() const { return ptr; }
+        size_t length() const { return len; }
+    };
+    BufferChain() = default;
+    BufferChain(void* data, size_t capacity, size_t size = 0) : segs_{Segment{data, size}}
+    {
+        (void)capacity;
+    }
+    void append(void* data, size_t size) { segs_.push_back(Segment{data, size}); }
+    std::vector<Segment>::const_iterator begin() const { return segs_.begin(); }
+    std::vector<Segment>::const_iterator end() const { return segs_.end(); }
+    void* readPtr() const { return segs_.empty() ? nullptr : segs_[0].ptr; }
+    size_t length() const { return segs_.empty() ? 0 : segs_[0].len; }
+    size_t chainLength() const  // kmbuffer.h:388-398
+    {
+        size_t n = 0;
+        for (const Segment& s : segs_) n += s.len;
+        return n;
+    }
+
+private:
+    std::vector<Segment> segs_;
+};
+
+using WSHandler = BasicWSHandler<FrameHeader, BufferChain, WSError, WSMode, int>;
+
+}  // namespace ws
+}  // namespace kmws
+
+#endif  // KMWS_WSHANDLER_HPP

@@ -39,3 +39,41 @@ def test_cpp_consumer_host_paths(tmp_path):
 def test_cpp_consumer_on_gpu(tmp_path):
     r = _build_and_run(tmp_path)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def _build_adapter(tmp_path, sanitize=False):
+    """tests/cpp/wshandler_adapter.cpp: include/kmws_wshandler.hpp (the C++
+    WSHandler drop-in) driven like WebSocket::Impl drives kuma's WSHandler."""
+    lib = kb.build()
+    exe = tmp_path / ("wsa_asan" if sanitize else "wsa")
+    flags = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"] if sanitize else ["-O2"]
+    subprocess.check_call(["g++", "-std=c++14", "-Wall", "-Wextra", "-Werror", *flags, "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "wshandler_adapter.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-o", str(exe)])
+    return exe
+
+
+def _no_device() -> bool:
+    from kuma_amd import kmws
+    return kmws.lib().kmws_device_count() == 0
+
+
+def test_wshandler_adapter_host(tmp_path):
+    """Header pack, CLIENT-mode decode, byte-at-a-time returns, CLOSE, reset and a
+    callback that deletes its handler (under ASan/UBSan); without a device a
+    masked frame must fail loudly (no CPU fallback)."""
+    exe = _build_adapter(tmp_path, sanitize=True)
+    mode = "nogpu" if _no_device() else ""
+    r = subprocess.run([str(exe), mode], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "ASAN_OPTIONS": "detect_leaks=0"})
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_wshandler_adapter_on_gpu(tmp_path):
+    """SERVER-mode masked frames unmasked in place on the GPU, the a-2 chain
+    vector, and a 16-fragment client message (a-10/a-12) decoded back."""
+    exe = _build_adapter(tmp_path)
+    r = subprocess.run([str(exe), "gpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
