@@ -47,6 +47,7 @@ __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __res
     const uint64_t b0 = (start + T - 1) >> tile_shift;
     const uint64_t b1 = (next + T - 1) >> tile_shift;
     for (uint64_t b = b0; b < b1; ++b) map[b] = f;
+    if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
 }
 
 // Issue every payload load of a tile.  Full tiles load unconditionally so the
@@ -68,11 +69,16 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint
 // Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
 template <int V, bool FULL>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
-                                            const kmws_desc* __restrict__ d, uint32_t n, uint32_t f, bool ok,
+                                            const kmws_desc* __restrict__ d, uint32_t n,
+                                            const uint32_t* __restrict__ map, uint32_t tile, bool ok,
                                             const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
 {
     using Cfg = UnmaskCfg<V>;
     const int tid = threadIdx.x;
+    // frames [f, flast] are the only ones that can overlap the tile: flast's
+    // region holds the next tile's start (the map's last entry is a sentinel)
+    uint32_t f = map[tile];
+    const uint32_t flast = map[tile + 1];
 
     // Fast path: one frame covers the whole tile (every tile of a 64 KiB-frame
     // arena).  The test reads block-uniform scalars only, so the branch is
@@ -96,7 +102,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
     for (;;) {
         const uint32_t fi = f + (uint32_t)tid;
         int valid = 0;
-        if (fi < n) {
+        if (fi < n && fi <= flast) {  // no descriptor loads past the tile's last frame
             const u32x4 x = *reinterpret_cast<const u32x4*>(d + fi);  // one 16-B load
             const uint64_t off = (uint64_t)x.x | ((uint64_t)x.y << 32);
             if (off < tile_hi) {
@@ -166,12 +172,12 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
     if (tile_lo + Cfg::kTile <= span) {
         load_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map[tile], head->status == 0, v, s_off,
+        finish_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off,
                              s_end, s_key);
     } else {
         load_tile<V, false>(base, tile_lo, span, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, false>(base, tile_lo, span, d, n, map[tile], head->status == 0, v, s_off, s_end, s_key);
+        finish_tile<V, false>(base, tile_lo, span, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
     }
 }
 
@@ -209,7 +215,7 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     u32x4 v[V];
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[tile], head->status == 0, v, s_off, s_end, s_key);
+    finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
 }
 
 // Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
@@ -235,7 +241,7 @@ __global__ void __launch_bounds__(kBlock) unmask_persist_kernel(uint8_t* __restr
         if (tn < nfull) load_tile<V, true>(base, (uint64_t)tn * Cfg::kTile, 0, w);
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t lo = (uint64_t)t * Cfg::kTile;
-        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[t], ok, v, s_off, s_end, s_key);
+        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, t, ok, v, s_off, s_end, s_key);
         if (tn >= nfull) break;
 #pragma unroll
         for (int i = 0; i < V; ++i) v[i] = w[i];
@@ -272,7 +278,7 @@ __global__ void __launch_bounds__(kBlock) unmask_pipe_kernel(uint8_t* __restrict
         const bool live = t < nfull;
         const uint32_t tt = live ? t : last;
         const uint64_t lo = (uint64_t)tt * Cfg::kTile;
-        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[tt], ok && live, vc, s_off, s_end, s_key);
+        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, tt, ok && live, vc, s_off, s_end, s_key);
         __builtin_amdgcn_sched_barrier(0);
         t = tn;
         return more;
@@ -335,7 +341,7 @@ __global__ void __launch_bounds__(kBlock) unmask_queue_kernel(uint8_t* __restric
             load_tile<V, true>(base, (uint64_t)(more ? tn : t) * Cfg::kTile, 0, vn);
             __builtin_amdgcn_sched_barrier(0);
             const uint64_t lo = (uint64_t)t * Cfg::kTile;
-            finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map[t], ok, vc, s_off, s_end, s_key);
+            finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, t, ok, vc, s_off, s_end, s_key);
             __builtin_amdgcn_sched_barrier(0);
             t = tn;
             return more;
@@ -448,7 +454,7 @@ static kmws_status check_ws(uint64_t span, size_t ws_bytes, uint64_t* ntiles_out
     using Cfg = UnmaskCfg<V>;
     const uint64_t ntiles = (span + Cfg::kTile - 1) / Cfg::kTile;
     if (ntiles > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
-    if (ws_bytes < sizeof(WsHead) + ntiles * sizeof(uint32_t)) return KMWS_ERR_BUFFER_TOO_SMALL;
+    if (ws_bytes < sizeof(WsHead) + (ntiles + 1) * sizeof(uint32_t)) return KMWS_ERR_BUFFER_TOO_SMALL;
     *ntiles_out = ntiles;
     return KMWS_OK;
 }
@@ -647,7 +653,7 @@ size_t kmws_unmask_workspace_size(uint64_t span)
 {
     // sized for the smallest tile any variant uses
     const uint64_t ntiles = (span + UnmaskCfg<4>::kTile - 1) / UnmaskCfg<4>::kTile;
-    return sizeof(WsHead) + (size_t)ntiles * sizeof(uint32_t);
+    return sizeof(WsHead) + (size_t)(ntiles + 1) * sizeof(uint32_t);  // + the map's sentinel
 }
 
 kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 V=${1:-0,8192,16384,24576,32768,65536,131072,2049,4097,8193,16385,32769,65537,131073,262145}
 M=${2:-sync}
 for k in 1 2; do
-  timeout -k 10 240 python tools/sweep_unmask.py "$V" 3 ${3:-3} $((1 << 20)) $M > "$OUT/sweep_$k.jsonl" 2> "$OUT/sweep_$k.err" || { tail -5 "$OUT/sweep_$k.err"; exit 1; }
+  timeout -k 10 240 python tools/sweep_unmask.py "$V" 3 ${3:-3} ${4:-$((1 << 20))} $M ${5:-65536} ${6:-${5:-65536}} > "$OUT/sweep_$k.jsonl" 2> "$OUT/sweep_$k.err" || { tail -5 "$OUT/sweep_$k.err"; exit 1; }
 done
 python - "$OUT" <<'PY'
 import json, sys

@@ -1,7 +1,8 @@
 """Interleaved A/B of unmask schedules in ONE process (one allocation):
 cfg2 (1 M x 64 KiB frames, device-resident), every variant timed with HIP
 events on the launch stream, `rounds` rounds of `reps` launches each.
-usage: python tools/sweep_unmask.py <variant,variant,...> [rounds] [reps] [frames] [sync|b2b]
+usage: python tools/sweep_unmask.py <variant,variant,...> [rounds] [reps] [frames] [sync|b2b] [stride] [len]
+(frame i's payload at i * stride, len bytes; default 64 KiB frames back to back)
 sync: every launch timed alone (synchronized); b2b: `reps` launches queued back
 to back and timed as one (as bench.py runs them), per-launch average.
 Variant numbers as kmws_unmask_batch_variant; >= 64 = a raw schedule code
@@ -22,12 +23,13 @@ def main():
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     n = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
     mode = sys.argv[5] if len(sys.argv) > 5 else "sync"
-    L = 65536
-    span = n * L
+    stride = int(sys.argv[6]) if len(sys.argv) > 6 else 65536
+    L = int(sys.argv[7]) if len(sys.argv) > 7 else stride
+    span = n * stride
     base = torch.empty(span, dtype=torch.uint8, device="cuda")
     descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
     kmws.fill_synthetic(base, 7)
-    kmws.fill_uniform_descs(descs, L, L, 11)
+    kmws.fill_uniform_descs(descs, stride, L, 11)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
     s = torch.cuda.current_stream()
     times = {v: [] for v in variants}
@@ -54,7 +56,8 @@ def main():
                 times[v].append(e0.elapsed_time(e1))
     assert ws.status() == 0
     alg = n * (2 * L + 16)
-    print(json.dumps({"resident_blocks": kmws.unmask_resident_blocks(), "frames": n, "mode": mode}), flush=True)
+    print(json.dumps({"resident_blocks": kmws.unmask_resident_blocks(), "frames": n, "mode": mode,
+                      "stride": stride, "len": L}), flush=True)
     for v in variants:
         med = statistics.median(times[v])
         print(json.dumps({"variant": v, "median_ms": round(med, 3), "min_ms": round(min(times[v]), 3),
