@@ -54,4 +54,24 @@ inline kmws_status hip_status(hipError_t e)
     return e == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
 }
 
+// Small host batches (the decoder's staging, kmws_unmask.hip): one block per
+// piece of at most kPieceWords 16-byte words of one frame's aligned hull.
+constexpr uint32_t kPieceWords = 4 * kBlock;  // 16 KiB
+struct PieceRec {
+    uint32_t frame;  // index into the descriptor list
+    uint32_t piece;  // piece of that frame's hull
+};
+// Pieces of a payload at byte offset `off`, `len` bytes (0 for an empty one).
+inline uint64_t piece_count(uint64_t off, uint32_t len)
+{
+    if (len == 0) return 0;
+    const uint64_t words = ((off + len + 15) >> 4) - (off >> 4);
+    return (words + kPieceWords - 1) / kPieceWords;
+}
+// Unmasks the payloads of descs[] (device-visible, sorted or not, disjoint)
+// in base[] with one launch over the np pieces; no plan, no validation (the
+// caller produced the descriptors).
+kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,
+                                 hipStream_t s);
+
 }  // namespace kmws

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "kmws_common.hpp"
 #include "kmws_gpu.h"
 
 namespace kmws {
@@ -53,9 +54,8 @@ inline size_t grow(size_t need, size_t have)
 }
 
 // A batch of payloads unmasked in place by the GPU.  Payloads are appended to
-// a pinned host area (16-B aligned starts, so whole-frame tiles take the
-// kernel's fast path); run() copies the descriptors to the device, launches
-// kmws_unmask_batch on the pinned area itself (zero-copy over PCIe) and waits.
+// a pinned host area (16-B aligned starts); run() launches the pieces kernel
+// on the pinned area itself (zero-copy over PCIe) and waits.
 // An optional second batch of descriptors can target another pinned buffer
 // (a caller's registered receive buffer).
 class PinnedStage {
@@ -119,82 +119,84 @@ public:
     }
 
     // Unmask every staged descriptor (and `extra` over `extra_base`, a pinned
-    // buffer of extra_span bytes, if given), then wait for the GPU.
+    // buffer of extra_span bytes, if given), then wait for the GPU.  One launch
+    // per buffer (launch_unmask_pieces) reading descriptors and piece list from
+    // pinned memory: no plan kernels, no copies, no status read-back.
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                     const std::vector<kmws_desc>* extra = nullptr)
     {
         const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
         if (n1 + n2 == 0) return KMWS_OK;
         DevGuard g(device_);
-        kmws_status st = ensure_dev(n1 + n2, std::max<uint64_t>((len_ + 15) & ~(size_t)15, extra_span));
+        // the extra buffer's 16-B aligned base, descriptors rebased onto it
+        uint8_t* eb = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(extra_base) & ~(uintptr_t)15);
+        const uint64_t delta = (uint64_t)(extra_base - eb);
+        uint64_t p1 = 0, p2 = 0;
+        for (const kmws_desc& x : descs_) p1 += piece_count(x.off, x.len);
+        for (size_t i = 0; i < n2; ++i) {
+            const kmws_desc& x = (*extra)[i];
+            if (x.off + x.len > extra_span) return KMWS_ERR_INVALID_PARAM;
+            p2 += piece_count(x.off + delta, x.len);
+        }
+        if (p1 + p2 > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+        kmws_status st = ensure_host(n1 + n2, p1 + p2);
         if (st != KMWS_OK) return st;
         std::memcpy(h_desc_, descs_.data(), n1 * sizeof(kmws_desc));
-        if (n2) std::memcpy(h_desc_ + n1, extra->data(), n2 * sizeof(kmws_desc));
-        if (n1 && hipMemcpyAsync(d_desc_, h_desc_, n1 * sizeof(kmws_desc), hipMemcpyHostToDevice, stream_) !=
-                      hipSuccess)
-            return KMWS_ERR_FAILED;
-        uint32_t status[2] = {0, 0};
-        if (n1) {
+        size_t k = 0;
+        for (size_t i = 0; i < n1; ++i)
+            for (uint64_t j = 0, c = piece_count(descs_[i].off, descs_[i].len); j < c; ++j)
+                h_piece_[k++] = PieceRec{(uint32_t)i, (uint32_t)j};
+        for (size_t i = 0; i < n2; ++i) {
+            kmws_desc x = (*extra)[i];
+            x.off += delta;
+            h_desc_[n1 + i] = x;
+            for (uint64_t j = 0, c = piece_count(x.off, x.len); j < c; ++j)
+                h_piece_[k++] = PieceRec{(uint32_t)i, (uint32_t)j};
+        }
+        if (p1) {
             uint8_t* dv = static_cast<uint8_t*>(device_view(h_));
             if (!dv) return KMWS_ERR_FAILED;
-            st = kmws_unmask_batch(dv, (len_ + 15) & ~(size_t)15, d_desc_, (uint32_t)n1, d_ws_[0], ws_cap_, stream_);
+            st = launch_unmask_pieces(dv, dv_desc_, dv_piece_, (uint32_t)p1, stream_);
             if (st != KMWS_OK) return st;
-            if (hipMemcpyAsync(&status[0], d_ws_[0], 4, hipMemcpyDeviceToHost, stream_) != hipSuccess)
-                return KMWS_ERR_FAILED;
         }
-        if (n2) {
-            // Only the extent the descriptors cover is processed: rebase them
-            // onto its 16-B aligned start (a large pinned ring may hold few frames).
-            uint64_t lo = ~0ull, hi = 0;
-            for (const kmws_desc& x : *extra) {
-                lo = std::min<uint64_t>(lo, x.off);
-                hi = std::max<uint64_t>(hi, x.off + x.len);
-            }
-            lo &= ~(uint64_t)15;
-            if (hi > extra_span) return KMWS_ERR_INVALID_PARAM;
-            for (size_t i = 0; i < n2; ++i) h_desc_[n1 + i].off -= lo;
-            if (hipMemcpyAsync(d_desc_ + n1, h_desc_ + n1, n2 * sizeof(kmws_desc), hipMemcpyHostToDevice, stream_) !=
-                hipSuccess)
-                return KMWS_ERR_FAILED;
-            uint8_t* dv = static_cast<uint8_t*>(device_view(extra_base));
+        if (p2) {
+            uint8_t* dv = static_cast<uint8_t*>(device_view(eb));
             if (!dv) return KMWS_ERR_INVALID_PARAM;
-            st = kmws_unmask_batch(dv + lo, hi - lo, d_desc_ + n1, (uint32_t)n2, d_ws_[1], ws_cap_, stream_);
+            st = launch_unmask_pieces(dv, dv_desc_ + n1, dv_piece_ + p1, (uint32_t)p2, stream_);
             if (st != KMWS_OK) return st;
-            if (hipMemcpyAsync(&status[1], d_ws_[1], 4, hipMemcpyDeviceToHost, stream_) != hipSuccess)
-                return KMWS_ERR_FAILED;
         }
-        if (hipStreamSynchronize(stream_) != hipSuccess) return KMWS_ERR_FAILED;
-        return (status[0] | status[1]) == 0 ? KMWS_OK : KMWS_ERR_INVALID_STATE;
+        return hipStreamSynchronize(stream_) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
     }
 
 private:
-    kmws_status ensure_dev(size_t nd, uint64_t span)
+    // Pinned descriptor and piece arrays (and their device views) for nd / np entries.
+    kmws_status ensure_host(size_t nd, size_t np)
     {
         if (nd > desc_cap_) {
             const size_t c = std::max<size_t>(nd * 2, 1024);
             if (h_desc_) (void)hipHostFree(h_desc_);
-            if (d_desc_) (void)hipFree(d_desc_);
             h_desc_ = nullptr;
-            d_desc_ = nullptr;
+            dv_desc_ = nullptr;
             desc_cap_ = 0;
             if (hipHostMalloc(reinterpret_cast<void**>(&h_desc_), c * sizeof(kmws_desc), hipHostMallocDefault) !=
-                    hipSuccess ||
-                hipMalloc(reinterpret_cast<void**>(&d_desc_), c * sizeof(kmws_desc)) != hipSuccess)
+                hipSuccess)
                 return KMWS_ERR_FAILED;
+            dv_desc_ = static_cast<kmws_desc*>(device_view(h_desc_));
+            if (!dv_desc_) return KMWS_ERR_FAILED;
             desc_cap_ = c;
         }
-        const size_t ws = kmws_unmask_workspace_size(span);
-        if (ws > ws_cap_) {
-            for (void*& w : d_ws_) {
-                if (w) (void)hipFree(w);
-                w = nullptr;
-            }
-            ws_cap_ = grow(ws, ws_cap_);
-            for (void*& w : d_ws_)
-                if (hipMalloc(&w, ws_cap_) != hipSuccess) {
-                    ws_cap_ = 0;
-                    return KMWS_ERR_FAILED;
-                }
+        if (np > piece_cap_) {
+            const size_t c = std::max<size_t>(np * 2, 1024);
+            if (h_piece_) (void)hipHostFree(h_piece_);
+            h_piece_ = nullptr;
+            dv_piece_ = nullptr;
+            piece_cap_ = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&h_piece_), c * sizeof(PieceRec), hipHostMallocDefault) !=
+                hipSuccess)
+                return KMWS_ERR_FAILED;
+            dv_piece_ = static_cast<PieceRec*>(device_view(h_piece_));
+            if (!dv_piece_) return KMWS_ERR_FAILED;
+            piece_cap_ = c;
         }
         return KMWS_OK;
     }
@@ -203,9 +205,7 @@ private:
         if (stream_) (void)hipStreamSynchronize(stream_);
         if (h_) (void)hipHostFree(h_);
         if (h_desc_) (void)hipHostFree(h_desc_);
-        if (d_desc_) (void)hipFree(d_desc_);
-        for (void* w : d_ws_)
-            if (w) (void)hipFree(w);
+        if (h_piece_) (void)hipHostFree(h_piece_);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
 
@@ -215,11 +215,12 @@ private:
     uint8_t* h_ = nullptr;
     size_t cap_ = 0, len_ = 0;
     std::vector<kmws_desc> descs_;
-    kmws_desc* h_desc_ = nullptr;
-    kmws_desc* d_desc_ = nullptr;
+    kmws_desc* h_desc_ = nullptr;   // pinned, read by the kernel over PCIe
+    kmws_desc* dv_desc_ = nullptr;  // its device view
     size_t desc_cap_ = 0;
-    void* d_ws_[2] = {nullptr, nullptr};
-    size_t ws_cap_ = 0;
+    PieceRec* h_piece_ = nullptr;
+    PieceRec* dv_piece_ = nullptr;
+    size_t piece_cap_ = 0;
 };
 
 }  // namespace kmws

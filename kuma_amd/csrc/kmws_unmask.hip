@@ -360,6 +360,50 @@ __global__ void __launch_bounds__(kBlock) unmask_queue_kernel(uint8_t* __restric
     }
 }
 
+// Small host batches: the decoder's payloads of one socket read or one loop
+// iteration, produced by its own parser (disjoint, in range: nothing to
+// validate).  A plan + apply per read costs more than the bytes, so these go
+// in ONE launch: block b unmasks piece pieces[b] -- up to kPieceWords words of
+// one frame's aligned hull -- with descriptors and piece list read from
+// host-visible memory.  A hull's first and last words may hold bytes of other
+// frames (or headers): those words are written byte by byte, the frame's own
+// bytes only, so blocks of neighbouring frames never write the same byte.
+__global__ void __launch_bounds__(kBlock) unmask_pieces_kernel(uint8_t* __restrict__ base,
+                                                               const kmws_desc* __restrict__ d,
+                                                               const PieceRec* __restrict__ pieces)
+{
+    constexpr int V = kPieceWords / kBlock;
+    const PieceRec pr = pieces[blockIdx.x];
+    const kmws_desc x = d[pr.frame];
+    const uint64_t end = x.off + x.len;
+    const uint64_t w0 = (x.off >> 4) + (uint64_t)pr.piece * kPieceWords;
+    const uint64_t wh = (end + 15) >> 4;
+    const uint64_t w1 = wh < w0 + kPieceWords ? wh : w0 + kPieceWords;
+    const uint32_t r = rot_key(x.key, x.off);
+    u32x4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint64_t w = w0 + threadIdx.x + (uint64_t)kBlock * i;
+        v[i] = w < w1 ? *reinterpret_cast<const u32x4*>(base + 16 * w) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint64_t w = w0 + threadIdx.x + (uint64_t)kBlock * i;
+        if (w >= w1) continue;
+        const uint64_t a = 16 * w;
+        if (a >= x.off && a + 16 <= end) {
+            *reinterpret_cast<u32x4*>(base + a) = v[i] ^ r;
+        } else {  // the hull's first or last word: own bytes only
+            const uint64_t lo = a > x.off ? a : x.off, hi = a + 16 < end ? a + 16 : end;
+            for (uint64_t q = lo; q < hi; ++q) {
+                const uint32_t b = (uint32_t)(q - a);
+                const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
+                base[q] = (uint8_t)((dw ^ r) >> (8 * (b & 3u)));
+            }
+        }
+    }
+}
+
 // ---- synthetic fill: byte i = byte (i & 7) of splitmix64(seed + (i >> 3)) ----
 __global__ void __launch_bounds__(kBlock) fill_synthetic_kernel(uint8_t* __restrict__ base, uint64_t bytes,
                                                                 uint64_t seed)
@@ -643,6 +687,14 @@ static bool bad_args(const uint8_t* base, const kmws_desc* descs, uint32_t n, co
     return !ws || (n && (!base || !descs)) || (reinterpret_cast<uintptr_t>(base) & 15u);
 }
 
+kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,
+                                 hipStream_t s)
+{
+    if (np == 0) return KMWS_OK;
+    if (!base || !descs || !pieces) return KMWS_ERR_INVALID_PARAM;
+    hipLaunchKernelGGL(unmask_pieces_kernel, dim3(np), dim3(kBlock), 0, s, base, descs, pieces);
+    return hip_status(hipGetLastError());
+}
 }  // namespace kmws
 
 using namespace kmws;
