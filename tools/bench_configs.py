@@ -312,14 +312,16 @@ def e2e(gib: float, chunk_mib: int, depth: int):
         rates[name] = n * L / sorted(ts)[1] / 2**30
         del p
     t = n * L / max(rates.values()) / 2**30
-    # 2 modes x (1 warm + 3) = 8 passes: even, so the payload is back to 0x5A
-    ok = bool((hv[int(offs[0]):int(offs[0]) + L] == 0x5A).all()) and bool((hv[int(offs[-1]):int(offs[-1]) + L] == 0x5A).all())
+    # 2 modes x (1 warm + 3) = 8 passes: even, so every byte (payloads, headers,
+    # the 16-B hulls the zero-copy kernel rewrites) is back to 0x5A
+    ok = bool((host == 0x5A).all())
     # raw PCIe copies for context
-    dbuf = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
-    hb = host[:1 << 30]
+    cb = min(1 << 30, span)
+    dbuf = torch.empty(cb, dtype=torch.uint8, device="cuda")
+    hb = host[:cb]
     torch.cuda.synchronize()
-    t0 = time.perf_counter(); dbuf.copy_(hb, non_blocking=True); torch.cuda.synchronize(); h2d = (1 << 30) / (time.perf_counter() - t0)
-    t0 = time.perf_counter(); hb.copy_(dbuf, non_blocking=True); torch.cuda.synchronize(); d2h = (1 << 30) / (time.perf_counter() - t0)
+    t0 = time.perf_counter(); dbuf.copy_(hb, non_blocking=True); torch.cuda.synchronize(); h2d = cb / (time.perf_counter() - t0)
+    t0 = time.perf_counter(); hb.copy_(dbuf, non_blocking=True); torch.cuda.synchronize(); d2h = cb / (time.perf_counter() - t0)
     return {"config": "e2e", "frames": n, "frame_len": L, "host_bytes": span, "chunk_MiB": chunk_mib,
             "depth": depth, "payload_GiB_s": n * L / t / 2**30, "by_transfer_GiB_s": rates,
             "pcie_h2d_GiB_s": h2d / 2**30, "pcie_d2h_GiB_s": d2h / 2**30, "verified": ok,
