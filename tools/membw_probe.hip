@@ -146,6 +146,23 @@ __global__ void __launch_bounds__(B) xor_split_nt(u32x4* p, uint32_t c)
     for (int i = 0; i < V; ++i) __builtin_nontemporal_store(v[i] ^ c, p + base + (uint64_t)B * i);
 }
 
+// xor_split_nt with plain (temporal) loads and/or stores
+template <int V, int B, int K, bool NTL, bool NTS>
+__global__ void __launch_bounds__(B) xor_split_pol(u32x4* p, uint32_t c)
+{
+    const uint64_t q = gridDim.x / K;
+    const uint64_t t = K > 1 ? (blockIdx.x % K) * q + blockIdx.x / K : blockIdx.x;
+    const uint64_t base = t * B * V + threadIdx.x;
+    u32x4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = NTL ? __builtin_nontemporal_load(p + base + (uint64_t)B * i) : p[base + (uint64_t)B * i];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        if (NTS) __builtin_nontemporal_store(v[i] ^ c, p + base + (uint64_t)B * i);
+        else p[base + (uint64_t)B * i] = v[i] ^ c;
+    }
+}
+
 // read-only ceiling: XOR-reduce a tile, one word per block out (negligible writes)
 template <int V, int B, int K>
 __global__ void __launch_bounds__(B) read_split_nt(const u32x4* p, u32x4* out)
@@ -233,6 +250,12 @@ int main(int argc, char** argv)
                 {"copy nt V4 (half -> half), in order", 44}, {"copy nt V4 (half -> half), split 8", 45},
                 {"xor nt V4, in order", 46}, {"xor nt V4, split 2", 47}, {"xor nt V4, split 8", 48},
                 {"product kmws_unmask_apply (default schedule)", 9}};
+    } else if (argc > 3 && std::string(argv[3]) == "split") {  // in-place XOR shapes under the split-8 mapping
+        vars = {{"xor nt V4 B256, split 8", 48}, {"xor nt V2 B256, split 8", 50}, {"xor nt V8 B256, split 8", 51},
+                {"xor nt V4 B512, split 8", 52}, {"xor nt V2 B512, split 8", 53}, {"xor nt V4 B128, split 8", 54},
+                {"xor plain-load nt-store V4, split 8", 55}, {"xor nt-load plain-store V4, split 8", 56},
+                {"xor plain V4, split 8", 57}, {"xor nt V4 B256, split 4", 58}, {"xor nt V8 B256, split 2", 59},
+                {"product kmws_unmask_apply (default schedule)", 9}};
     } else if (argc > 3) {  // "product": only the product variants, interleaved
         std::vector<Var> keep;
         for (auto& v : vars)
@@ -290,6 +313,16 @@ int main(int argc, char** argv)
             case 46: hipLaunchKernelGGL((xor_split_nt<4, 256, 1>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
             case 47: hipLaunchKernelGGL((xor_split_nt<4, 256, 2>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
             case 48: hipLaunchKernelGGL((xor_split_nt<4, 256, 8>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 50: hipLaunchKernelGGL((xor_split_nt<2, 256, 8>), dim3(nw / 512), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 51: hipLaunchKernelGGL((xor_split_nt<8, 256, 8>), dim3(nw / 2048), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 52: hipLaunchKernelGGL((xor_split_nt<4, 512, 8>), dim3(nw / 2048), dim3(512), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 53: hipLaunchKernelGGL((xor_split_nt<2, 512, 8>), dim3(nw / 1024), dim3(512), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 54: hipLaunchKernelGGL((xor_split_nt<4, 128, 8>), dim3(nw / 512), dim3(128), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 55: hipLaunchKernelGGL((xor_split_pol<4, 256, 8, false, true>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 56: hipLaunchKernelGGL((xor_split_pol<4, 256, 8, true, false>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 57: hipLaunchKernelGGL((xor_split_pol<4, 256, 8, false, false>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 58: hipLaunchKernelGGL((xor_split_nt<4, 256, 4>), dim3(nw / 1024), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
+            case 59: hipLaunchKernelGGL((xor_split_nt<8, 256, 2>), dim3(nw / 2048), dim3(256), 0, 0, (u32x4*)buf, 0x5au); break;
             }
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
