@@ -270,10 +270,12 @@ typedef struct kmws_pipeline kmws_pipeline;
 kmws_pipeline* kmws_pipeline_create(int device, uint64_t chunk_bytes, uint32_t max_frames_per_chunk, int depth);
 void           kmws_pipeline_destroy(kmws_pipeline* p);
 
-/* Transfer mode: AUTO = zero-copy when host_base is pinned (hipHostMalloc /
- * hipHostRegister; the kernel reads and writes host memory over PCIe), else
- * chunked SDMA copies through device slots; COPY forces the chunked SDMA
- * path; ZEROCOPY requires pinned memory. */
+/* Transfer mode: AUTO = chunked SDMA copies through device slots (H2D, kernel
+ * and D2H on three streams, so both DMA directions run at once), except for a
+ * pinned host_base (hipHostMalloc / hipHostRegister) spanning less than two
+ * chunks, which gets one zero-copy launch (the kernel reads and writes host
+ * memory over PCIe); COPY forces the chunked SDMA path; ZEROCOPY requires
+ * pinned memory.  At most 3 slots are used at once whatever the depth. */
 enum kmws_xfer { KMWS_XFER_AUTO = 0, KMWS_XFER_COPY = 1, KMWS_XFER_ZEROCOPY = 2 };
 kmws_status kmws_pipeline_set_transfer(kmws_pipeline* p, int mode);
 

@@ -1,10 +1,10 @@
 // Host-resident batches for kmws: the receive path starts and ends in host
 // memory (TcpConnection.cpp:229 reads sockets into a 64 KiB host buffer).
-//   - pinned host buffers: ONE zero-copy unmask launch that reads and writes
-//     the host bytes over PCIe (measured 41-44 GiB/s on MI355X, at the
-//     ~45 GiB/s per-direction ceiling of concurrent copies);
-//   - pageable buffers (or KMWS_XFER_COPY): a multi-slot ring of SDMA copies
-//     H2D -> unmask -> D2H, chunks cut on frame boundaries.
+//   - pinned host buffers under two chunks: ONE zero-copy unmask launch that
+//     reads and writes the host bytes over PCIe (41.8 GiB/s on MI355X);
+//   - pageable buffers, pinned batches of two chunks or more, or
+//     KMWS_XFER_COPY: a ring of SDMA copies H2D -> unmask -> D2H on three
+//     streams, chunks cut on frame boundaries (43-45 GiB/s on pinned memory).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,9 +18,15 @@
 using namespace kmws;
 
 struct kmws_pipeline {
+    // Copy ring: a slot's chunk goes H2D on s_in, is unmasked on s_kern and
+    // goes D2H on s_out, ordered by events.  One stream per direction keeps
+    // the copies of a direction back to back and lets H2D of chunk k+1 run
+    // beside D2H of chunk k (two DMA directions at once: 90 GiB/s on MI355X vs
+    // 53 for one); three streams stay within the 4 hardware queues a process
+    // gets, where a stream per slot would share queues and serialize.
+    hipStream_t s_in = nullptr, s_kern = nullptr, s_out = nullptr;
     struct Slot {
-        hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
+        hipEvent_t in_done = nullptr, kern_done = nullptr, done = nullptr;
         uint8_t* d_buf = nullptr;
         kmws_desc* d_desc = nullptr;
         kmws_desc* h_desc = nullptr;  // pinned staging for rebased descriptors
@@ -42,15 +48,18 @@ struct kmws_pipeline {
     {
         if (zc_desc) (void)hipFree(zc_desc);
         if (zc_ws) (void)hipFree(zc_ws);
+        for (hipStream_t st : {s_in, s_kern, s_out})
+            if (st) (void)hipStreamSynchronize(st);
         for (Slot& s : slots) {
-            if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.d_buf) (void)hipFree(s.d_buf);
             if (s.d_desc) (void)hipFree(s.d_desc);
             if (s.h_desc) (void)hipHostFree(s.h_desc);
             if (s.d_ws) (void)hipFree(s.d_ws);
-            if (s.done) (void)hipEventDestroy(s.done);
-            if (s.stream) (void)hipStreamDestroy(s.stream);
+            for (hipEvent_t e : {s.in_done, s.kern_done, s.done})
+                if (e) (void)hipEventDestroy(e);
         }
+        for (hipStream_t st : {s_in, s_kern, s_out})
+            if (st) (void)hipStreamDestroy(st);
     }
 };
 
@@ -69,9 +78,15 @@ kmws_pipeline* kmws_pipeline_create(int device, uint64_t chunk_bytes, uint32_t m
     p->max_frames = max_frames_per_chunk;
     p->slots.resize(depth);
     const uint64_t dev_bytes = p->chunk + 32;  // + alignment slack at both ends
+    for (hipStream_t* st : {&p->s_in, &p->s_kern, &p->s_out})
+        if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
+            delete p;
+            return nullptr;
+        }
     for (auto& s : p->slots) {
         s.ws_bytes = kmws_unmask_workspace_size(dev_bytes);
-        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+        if (hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.kern_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.d_buf), dev_bytes) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&s.d_desc), (size_t)p->max_frames * sizeof(kmws_desc)) != hipSuccess ||
@@ -108,9 +123,13 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
     if (n == 0) return KMWS_OK;
     uint8_t* dv = p->xfer == KMWS_XFER_COPY ? nullptr : static_cast<uint8_t*>(device_view(host_base));
     if (p->xfer == KMWS_XFER_ZEROCOPY && !dv) return KMWS_ERR_INVALID_PARAM;  // needs pinned memory
+    // AUTO on pinned memory: the copy ring once the batch spans two chunks (its
+    // two DMA directions overlap: 43-45 GiB/s vs 41.8 for the zero-copy kernel,
+    // profiles/r01e_e2e_ring.txt), the single zero-copy launch below that.
+    if (p->xfer == KMWS_XFER_AUTO && dv && span >= 2 * p->chunk) dv = nullptr;
     if (dv) {
         // Pinned host memory: one zero-copy unmask over PCIe, in place.
-        kmws_pipeline::Slot& s = p->slots[0];
+        hipStream_t zs = p->s_kern;
         if (n > p->zc_desc_cap) {
             if (p->zc_desc) (void)hipFree(p->zc_desc);
             p->zc_desc = nullptr;
@@ -127,14 +146,14 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
             if (hipMalloc(&p->zc_ws, ws) != hipSuccess) return KMWS_ERR_FAILED;
             p->zc_ws_cap = ws;
         }
-        if (hipMemcpyAsync(p->zc_desc, descs, (size_t)n * sizeof(kmws_desc), hipMemcpyHostToDevice, s.stream) !=
+        if (hipMemcpyAsync(p->zc_desc, descs, (size_t)n * sizeof(kmws_desc), hipMemcpyHostToDevice, zs) !=
             hipSuccess)
             return KMWS_ERR_FAILED;
-        kmws_status st = kmws_unmask_batch(dv, span, p->zc_desc, n, p->zc_ws, p->zc_ws_cap, s.stream);
+        kmws_status st = kmws_unmask_batch(dv, span, p->zc_desc, n, p->zc_ws, p->zc_ws_cap, zs);
         if (st != KMWS_OK) return st;
         uint32_t status = 0;
-        if (hipMemcpyAsync(&status, p->zc_ws, sizeof(status), hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
-            hipStreamSynchronize(s.stream) != hipSuccess)
+        if (hipMemcpyAsync(&status, p->zc_ws, sizeof(status), hipMemcpyDeviceToHost, zs) != hipSuccess ||
+            hipStreamSynchronize(zs) != hipSuccess)
             return KMWS_ERR_FAILED;
         return status == 0 ? KMWS_OK : KMWS_ERR_INVALID_PARAM;
     }
@@ -155,7 +174,9 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
             ++e;
         }
         if (e == f) return KMWS_ERR_BUFFER_TOO_SMALL;  // one frame larger than a chunk
-        kmws_pipeline::Slot& s = p->slots[k % p->slots.size()];
+        // at most 3 slots in flight: with 4, H2D runs far enough ahead to hold
+        // the DMA engines the D2H needs (26 GiB/s instead of 45)
+        kmws_pipeline::Slot& s = p->slots[k % std::min<size_t>(p->slots.size(), 3)];
         if (s.busy && hipEventSynchronize(s.done) != hipSuccess) return KMWS_ERR_FAILED;
         s.busy = false;
         const uint64_t first = descs[f].off;
@@ -165,16 +186,20 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
         }
         const uint64_t bytes = (hi + 15 - lo) & ~(uint64_t)15;
         const uint64_t h2d = hi - lo;  // never read past the caller's span
-        if (hipMemcpyAsync(s.d_buf, host_base + lo, h2d, hipMemcpyHostToDevice, s.stream) != hipSuccess ||
+        if (hipMemcpyAsync(s.d_buf, host_base + lo, h2d, hipMemcpyHostToDevice, p->s_in) != hipSuccess ||
             hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)(e - f) * sizeof(kmws_desc), hipMemcpyHostToDevice,
-                           s.stream) != hipSuccess)
+                           p->s_in) != hipSuccess ||
+            hipEventRecord(s.in_done, p->s_in) != hipSuccess ||
+            hipStreamWaitEvent(p->s_kern, s.in_done, 0) != hipSuccess)
             return KMWS_ERR_FAILED;
-        st = kmws_unmask_batch(s.d_buf, bytes, s.d_desc, e - f, s.d_ws, s.ws_bytes, s.stream);
+        st = kmws_unmask_batch(s.d_buf, bytes, s.d_desc, e - f, s.d_ws, s.ws_bytes, p->s_kern);
         if (st != KMWS_OK) break;
         // write back exactly the frames' extent: neighbours' bytes stay untouched
-        if (hipMemcpyAsync(host_base + first, s.d_buf + (first - lo), hi - first, hipMemcpyDeviceToHost,
-                           s.stream) != hipSuccess ||
-            hipEventRecord(s.done, s.stream) != hipSuccess)
+        if (hipEventRecord(s.kern_done, p->s_kern) != hipSuccess ||
+            hipStreamWaitEvent(p->s_out, s.kern_done, 0) != hipSuccess ||
+            hipMemcpyAsync(host_base + first, s.d_buf + (first - lo), hi - first, hipMemcpyDeviceToHost,
+                           p->s_out) != hipSuccess ||
+            hipEventRecord(s.done, p->s_out) != hipSuccess)
             return KMWS_ERR_FAILED;
         s.busy = true;
         f = e;

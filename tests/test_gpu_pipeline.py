@@ -39,16 +39,18 @@ def test_pipeline_pageable(kmws, chunk, max_frames, depth):
     assert np.array_equal(buf, want)
 
 
-@pytest.mark.parametrize("transfer", [0, 1, 2])
-def test_pipeline_pinned(kmws, transfer):
-    """AUTO/ZEROCOPY: the kernel works on pinned host memory over PCIe; COPY: SDMA ring."""
+@pytest.mark.parametrize("transfer,chunk,depth", [(0, 8 << 20, 3), (0, 256 << 20, 3), (1, 8 << 20, 8), (2, 8 << 20, 3)])
+def test_pipeline_pinned(kmws, transfer, chunk, depth):
+    """ZEROCOPY (and AUTO under two chunks): the kernel works on pinned host
+    memory over PCIe; COPY (and AUTO from two chunks): the 3-stream SDMA ring,
+    at most 3 slots in flight whatever the depth."""
     import torch
-    rng = np.random.default_rng(9 + transfer)
+    rng = np.random.default_rng(9 + transfer + depth + (chunk >> 20))
     buf, d = wire_like(rng, 3000, 70000)
     want = buf.copy()
     orc.unmask_batch(want, d)
     t = torch.from_numpy(buf).pin_memory()
-    kmws.Pipeline(0, 8 << 20, 4096, 3, transfer=transfer).unmask(t, d)
+    kmws.Pipeline(0, chunk, 4096, depth, transfer=transfer).unmask(t, d)
     assert np.array_equal(t.numpy(), want)
 
 
