@@ -547,7 +547,7 @@ __global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __rest
 // A frame's edge words -- its owned words outside its interior: q < head_f at
 // olo + q, then the tail at ihi + (q - head_f) -- composed one thread per
 // (frame, q) into edge[f * kEdgeWords + q].
-constexpr int kEdgeFramesPerBlock = kBlock / kEdgeWords;  // 28 frames, 252 threads
+constexpr int kEdgeFramesPerBlock = kBlock / kEdgeWords;  // 51 frames, 255 threads
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) edge_kernel(const uint8_t* __restrict__ src,
                                                       const uint64_t* __restrict__ start,
