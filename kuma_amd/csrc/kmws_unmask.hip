@@ -187,13 +187,14 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
 // blocks past k * (nfull / k) take the remaining tiles in order).  With c > 0
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
-// its own runs).
+// its own runs), inside w windows far apart (consecutive blocks of a residue
+// alternate between the windows).
 template <int V>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t k, uint32_t c, uint32_t b0)
+                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -204,11 +205,13 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     if (c == 0) {  // k equal parts
         const uint32_t q = nfull / k;
         if (b < q * k) tile = (b % k) * q + b / k;
-    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k
+    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k, in w windows
         const uint64_t run = (uint64_t)k * c;
-        if (b < nfull / run * run) {
+        const uint64_t per = (uint64_t)nfull / w / run * run;  // tiles per window
+        if (b < per * w) {
             const uint32_t x = b % k, i = b / k;
-            tile = (i / c) * (uint32_t)run + x * c + i % c;
+            const uint32_t j = i % w, i2 = i / w;  // window, position in the residue's stream
+            tile = (uint32_t)(j * per) + (i2 / c) * (uint32_t)run + x * c + i2 % c;
         }
     }
     const uint64_t lo = (uint64_t)tile * Cfg::kTile;
@@ -476,11 +479,13 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
 // Tile geometry used by the product path (tuned on MI355X).
 constexpr int kUnmaskV = 4;
 
-// Apply schedule per device (codes: launch_schedule).  Default 0: one block per
-// 16 KiB tile, consecutive blocks dealt over 8 parts of the span, so the blocks
-// in flight stream 8 windows far apart: 82-83 % of HBM peak where the in-order
-// grid gets 74.5-75 % (profiles/r01c_unmask_schedules.txt).  Set only by
-// kmws_unmask_autotune.
+// Apply schedule per device (codes: launch_schedule).  Where the blocks in
+// flight are decides the rate: the in-order grid streams one 16 MiB window
+// (74.5-75 % of HBM peak everywhere); dealing blocks over 8 parts of the span
+// streams 8 windows far apart (82-83 % on some 64 GiB placements in HBM, 76 %
+// on others); runs of 16 tiles per XCD hold 78-79 % on every placement and 82 %
+// on 4 KiB frames (profiles/r01f_unmask_placement.txt).  Default: XCD runs;
+// kmws_unmask_autotune picks per device on the caller's batch.
 constexpr int kMaxDevices = 64;
 static uint32_t g_schedule[kMaxDevices];
 using ProdCfg = UnmaskCfg<kUnmaskV>;
@@ -627,7 +632,7 @@ static kmws_status launch_apply_queue(uint8_t* base, uint64_t span, const kmws_d
 template <int V>
 static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
-                                      uint32_t c = 0)
+                                      uint32_t c = 0, uint32_t w = 1)
 {
     using Cfg = UnmaskCfg<V>;
     uint64_t ntiles = 0;
@@ -643,7 +648,7 @@ static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_d
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
         hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
-                           head, (uint32_t)nfull, k, c, (uint32_t)b0);
+                           head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
@@ -660,16 +665,17 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
 }
 
-// Schedule code: one block per tile with the tiles dealt over 8 parts of the
-// span (0, the default), in order (1), or over 2 parts (2); codes >= 64: a
-// persistent grid of that many blocks, grid-stride (even) or software-pipelined
-// (odd, grid = code - 1).
+// Schedule code, one block per 16 KiB tile: runs of 16 tiles per XCD (0, the
+// default), in order (1), tiles dealt over 2 parts of the span (2) or over 8
+// parts (3); codes >= 64: a persistent grid of that many blocks, grid-stride
+// (even) or software-pipelined (odd, grid = code - 1).
 static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                    const void* workspace, size_t ws_bytes, hipStream_t s)
 {
-    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
+    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
     if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
     if (code == 2) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 2u);
+    if (code == 3) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
     if (code < 64) return KMWS_ERR_INVALID_PARAM;
     if (code & 1u) return launch_apply_pipe<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code & ~1u);
     return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code);
@@ -751,9 +757,9 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     hipStream_t s = static_cast<hipStream_t>(stream);
     kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    // one block per tile dealt over 8 / 2 parts, in order; persistent 2 M blocks
-    // (2 tiles each); pipelined 64 K blocks (profiles/r01c_unmask_schedules.txt)
-    static const uint32_t cand[] = {0u, 2u, 1u, 2097152u, 65536u | 1u};
+    // XCD runs, 8 parts, 2 parts, in order: which wins depends on where the batch
+    // lies in HBM and on its frame layout (profiles/r01f_unmask_placement.txt)
+    static const uint32_t cand[] = {0u, 3u, 2u, 1u};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {
@@ -856,11 +862,11 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
     case 26:
     case 27:
     case 28:
-    case 29: {  // 16 KiB tiles, one block per tile, runs of 16 / 128 / 1024 / 8192 / 65536 tiles per XCD residue
+    case 29: {  // 16 KiB tiles, one block per tile, runs of 4 / 8 / 16 / 32 / 128 tiles per XCD residue
         kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
         if (st != KMWS_OK) return st;
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u,
-                                     16u << (3 * (variant - 25)));
+        static const uint32_t runs[] = {4u, 8u, 16u, 32u, 128u};
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, runs[variant - 25]);
     }
     case 30:
     case 31:
@@ -876,6 +882,26 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
         if (st != KMWS_OK) return st;
         return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, variant == 34 ? 2u : 8u);
+    }
+    case 40:
+    case 41:
+    case 42:
+    case 43:
+    case 44:
+    case 45:
+    case 46:
+    case 47: {  // runs of c tiles per XCD residue, in w far-apart windows: (c, w) below
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        static const uint32_t cw[][2] = {{16, 2}, {16, 4}, {16, 8}, {128, 2}, {128, 8}, {4, 8}, {1, 8}, {16, 16}};
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, cw[variant - 40][0],
+                                     cw[variant - 40][1]);
+    }
+    case 48:
+    case 49: {  // 32 KiB tiles, runs of 8 / 16 tiles per XCD residue
+        kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, 8u, variant == 48 ? 8u : 16u);
     }
     default:
         if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)
@@ -894,6 +920,38 @@ kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* 
     hipError_t e = hipMemcpyAsync(status_out, workspace, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return hip_status(e);
+}
+
+void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous)
+{
+    if (contiguous) *contiguous = 0;
+    if (bytes == 0) return nullptr;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return nullptr;
+    if (device != prev && hipSetDevice(device) != hipSuccess) return nullptr;
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+        if (contiguous) *contiguous = 1;
+    } else {
+        (void)hipGetLastError();
+        p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+        }
+    }
+    if (device != prev) (void)hipSetDevice(prev);
+    return p;
+}
+
+void kmws_arena_free(void* p, int device)
+{
+    if (!p) return;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return;
+    if (device != prev) (void)hipSetDevice(device);
+    (void)hipFree(p);
+    if (device != prev) (void)hipSetDevice(prev);
 }
 
 kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream)

@@ -37,7 +37,7 @@ EXPORTS = [
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
-    "kmws_rx_batch_attach_ring",
+    "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free",
 ]
 
 
@@ -101,6 +101,8 @@ def lib() -> C.CDLL:
         "kmws_unmask_batch_variant": (i32, [u8p, u64, vp, u32, vp, sz, vp, i32]),
         "kmws_read_status": (i32, [vp, C.POINTER(C.c_uint32), vp]),
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
+        "kmws_arena_alloc": (vp, [u64, i32, C.POINTER(C.c_int)]),
+        "kmws_arena_free": (None, [vp, i32]),
         "kmws_fill_uniform_descs": (i32, [vp, u32, u64, u32, u64, vp]),
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
@@ -331,6 +333,33 @@ class Workspace:
         out = C.c_uint32(0)
         _check(lib().kmws_read_status(self.ptr, C.byref(out), _stream_handle(stream)), "kmws_read_status")
         return out.value
+
+
+class Arena:
+    """kmws_arena_alloc: a device payload arena, physically contiguous when the
+    device can provide it.  `.tensor` is a uint8 torch view of it (through
+    __cuda_array_interface__); keep the Arena alive while the view is used."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        import torch
+        flag = C.c_int(0)
+        p = lib().kmws_arena_alloc(int(nbytes), device, C.byref(flag))
+        if not p:
+            raise RuntimeError(f"kmws_arena_alloc({nbytes}) failed")
+        self._p, self._dev, self.nbytes, self.contiguous = p, device, int(nbytes), bool(flag.value)
+        self.__cuda_array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1", "data": (p, False),
+                                         "version": 2, "strides": None}
+        self.tensor = torch.as_tensor(self, device=torch.device("cuda", device))
+        assert self.tensor.data_ptr() == p
+
+    def __del__(self):
+        try:
+            if getattr(self, "_p", None):
+                self.tensor = None
+                lib().kmws_arena_free(self._p, self._dev)
+                self._p = None
+        except Exception:
+            pass
 
 
 def unmask_workspace_size(span: int) -> int:

@@ -11,6 +11,7 @@ import json
 import statistics
 import sys
 import os
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -36,6 +37,7 @@ def main():
     for v in variants:  # warm every variant once
         kmws.unmask_batch(base, descs, ws, span, variant=v)
     torch.cuda.synchronize()
+    t_start = time.perf_counter()
     for _ in range(rounds):
         for v in variants:
             if mode == "b2b":
@@ -46,6 +48,9 @@ def main():
                 e1.record(s)
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) / reps)
+                if os.environ.get("SWEEP_TRACE"):
+                    print(json.dumps({"t": round(time.perf_counter() - t_start, 3), "variant": v,
+                                      "ms": round(times[v][-1], 3)}), flush=True)
                 continue
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
