@@ -730,8 +730,15 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // consecutive blocks dealt over `split` parts of the unit slots, so the
     // blocks in flight stream that many windows of the output far apart
-    const uint32_t q = gridDim.x / split;
-    const uint32_t b = blockIdx.x < q * split ? (blockIdx.x % split) * q + blockIdx.x / split : blockIdx.x;
+    // (split >= 1000: runs of split - 1000 blocks per XCD residue instead)
+    uint32_t b = blockIdx.x;
+    if (split >= 1000u) {
+        const uint32_t c = split - 1000u, run = 8u * c;
+        if (b < gridDim.x / run * run) b = (b / 8u / c) * run + (b % 8u) * c + (b / 8u) % c;
+    } else {
+        const uint32_t q = gridDim.x / split;
+        if (b < q * split) b = (b % split) * q + b / split;
+    }
     const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
     // record, slot count, status and total are independent scalar loads (one
     // latency level); slots past the count lie inside the workspace and are ignored

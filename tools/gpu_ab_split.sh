@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/abs
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-KMWS_COPY_SPLIT=8 timeout -k 10 300 python -u -m pytest tests/test_gpu_pack.py tests/test_gpu_decoder.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+KMWS_COPY_SPLIT=1016 timeout -k 10 300 python -u -m pytest tests/test_gpu_pack.py tests/test_gpu_decoder.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 for rep in 1 2; do
 for k in ${1:-1 2 8 16}; do
