@@ -106,19 +106,23 @@ def schedule_name(schedule: int) -> str:
     return f"{kind}, {schedule & ~1} blocks"
 
 
-def traffic_from_profile(frames: int, frame_len: int, kernel: str):
-    """HBM bytes per launch of the unmask kernel from the committed PMC pass
-    (profiles/*traffic*.json, written by tools/pmc_traffic.py), if it was
-    measured on this exact configuration; else None."""
+def traffic_from_profile(frames: int, frame_len: int, kernel: str, schedule=None):
+    """HBM bytes per launch of the unmask kernel from the committed PMC passes
+    (profiles/*traffic*.json, written by tools/pmc_traffic.py) measured on this
+    exact configuration: the latest one for this schedule if there is one, else
+    the latest for the kernel; None if there is none."""
     import glob
-    best = None
+    same, any_ = None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
         if t.get("frames") == frames and t.get("frame_len") == frame_len and t.get("kernel") == kernel:
-            best = t
+            any_ = t
+            if schedule is not None and t.get("schedule") == schedule:
+                same = t
+    best = same or any_
     return None if best is None else best.get("hbm_bytes_per_launch")
 
 
@@ -222,7 +226,7 @@ def main():
     alg_bytes = n * (2 * L + DESC_BYTES)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kernel = schedule_kernel(schedule) if variant is None else f"kmws_unmask_batch_variant({variant})"
-    traffic = traffic_from_profile(n, L, kernel)
+    traffic = traffic_from_profile(n, L, kernel, schedule if variant is None else None)
 
     out = None
     if rank == 0:

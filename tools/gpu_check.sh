@@ -13,7 +13,7 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
 echo "gpu tests ok" && tail -2 "$OUT/pytest_gpu.log" &&
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --cpu-seconds 10 > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 cat "$OUT/bench.json" &&
-for v in 0 21; do
+for v in 0 23 27; do
   timeout -k 10 200 python bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-verify --variant $v > "$OUT/bench_v$v.json" 2>> "$OUT/bench.err" || exit 1
   python -c "import json;d=json.load(open('$OUT/bench_v$v.json'));print('variant $v', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done &&

@@ -14,7 +14,10 @@ pass() {  # name counter bench-args
 }
 pass split_fetch FETCH_SIZE "--no-autotune" &&
 pass split_write WRITE_SIZE "--no-autotune" &&
-python3 tools/pmc_traffic.py "$OUT/split_fetch" "$OUT/split_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split.json" &&
+python3 tools/pmc_traffic.py "$OUT/split_fetch" "$OUT/split_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split.json" 0 &&
+pass split8_fetch FETCH_SIZE "--variant 23" &&
+pass split8_write WRITE_SIZE "--variant 23" &&
+python3 tools/pmc_traffic.py "$OUT/split8_fetch" "$OUT/split8_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split8.json" 3 &&
 pass tiles_fetch FETCH_SIZE "--variant 0" &&
 pass tiles_write WRITE_SIZE "--variant 0" &&
 python3 tools/pmc_traffic.py "$OUT/tiles_fetch" "$OUT/tiles_write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json" &&

@@ -36,6 +36,7 @@ def per_dispatch(rows, counter, kern):
 
 def main():
     fdir, wdir, kern, frames, flen, out = sys.argv[1:7]
+    schedule = int(sys.argv[7]) if len(sys.argv) > 7 else None  # kmws_unmask_schedule() code of the pass
     frames, flen = int(frames), int(flen)
     f = per_dispatch(counter_rows(fdir), "FETCH_SIZE", kern)
     w = per_dispatch(counter_rows(wdir), "WRITE_SIZE", kern)
@@ -51,6 +52,8 @@ def main():
            "hbm_bytes_per_launch": read_bytes + write_bytes, "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": (read_bytes + write_bytes) / alg,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB->bytes x1024"}
+    if schedule is not None:
+        res["schedule"] = schedule
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
