@@ -135,3 +135,15 @@ def test_find_headers_matches_oracle_walk():
     # invalid 127-class length is recorded and ends the walk
     got, _ = kmws.find_headers(bytes.fromhex("827f4000000000000000") + stream)
     assert got == [0]
+
+
+def test_arena_alloc_without_device_returns_null():
+    """No gfx950 device here: kmws_arena_alloc reports failure (NULL), no crash."""
+    import ctypes as C
+    from kuma_amd import kmws
+    if kmws.lib().kmws_device_count() > 0:
+        pytest.skip("a device is present")
+    flag = C.c_int(7)
+    assert not kmws.lib().kmws_arena_alloc(1 << 20, 0, C.byref(flag))
+    assert flag.value == 0
+    kmws.lib().kmws_arena_free(None, 0)

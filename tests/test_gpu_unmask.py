@@ -233,3 +233,22 @@ def test_resident_blocks_reported(torch_dev):
     from kuma_amd import kmws
     r = kmws.unmask_resident_blocks()
     assert r > 0 and r % torch_dev.cuda.get_device_properties(0).multi_processor_count == 0
+
+
+def test_arena_alloc_unmask_roundtrip(torch_dev):
+    """kmws_arena_alloc: a (physically contiguous where possible) arena usable
+    as a torch view; unmask on it, checked on the device; freed without error."""
+    torch = torch_dev
+    from kuma_amd import kmws
+    span, L = 256 << 20, 65536
+    a = kmws.Arena(span)
+    assert a.tensor.data_ptr() == a._p and a.tensor.numel() == span
+    descs = torch.empty((span // L, 2), dtype=torch.int64, device="cuda")
+    kmws.fill_synthetic(a.tensor, 77)
+    kmws.fill_uniform_descs(descs, L, L - 5, 5)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span))
+    kmws.unmask_batch(a.tensor, descs, ws, span)
+    torch.cuda.synchronize()
+    assert ws.status() == 0 and kmws.check_unmasked(a.tensor, 77, descs) == 0
+    del a
+    torch.cuda.synchronize()
