@@ -200,14 +200,10 @@ int kmws_unmask_resident_blocks(void);
  * 16 KiB tiles on a persistent grid-stride grid of 8 K (3), 16 K (4), 24 K (5),
  * 32 K (6) or 64 K (7) blocks; one block per tile with registers capped for 6 (8)
  * or 8 (9) waves per SIMD; pipelined persistent grid of 16 K (10), 32 K (11) or
- * 64 K (12) blocks; work queue (one resident grid taking chunks of 1 (13), 4 (14)
- * or 16 (15) tiles; chunks of 4 on twice the resident grid (16)); pipelined grid
- * of 1, 2, 4 or 8 x the resident blocks (17-20); one block per 16 KiB tile dealt
- * over 2, 4, 8, 16 (21-24) or 3, 6, 12, 32 (30-33) parts of the span, or in runs
- * of 4, 8, 16, 32, 128 tiles over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8
- * parts (34, 35); XCD runs of (16, 16, 16, 128, 128, 4, 1, 16) tiles inside (2, 4,
- * 8, 2, 8, 8, 8, 16) far-apart windows (40-47); 32 KiB tiles in XCD runs of 8 / 16
- * (48, 49); any value >= 64: a schedule code as kmws_unmask_schedule() returns. */
+ * 64 K (12) blocks; one block per 16 KiB tile dealt over 2, 4, 8, 16 (21-24) or
+ * 3, 6, 12, 32 (30-33) parts of the span, or in runs of 4, 8, 16, 32, 128 tiles
+ * over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8 parts (34, 35); any value
+ * >= 64: a schedule code as kmws_unmask_schedule() returns. */
 kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       void* workspace, size_t workspace_bytes, void* stream, int variant);
 

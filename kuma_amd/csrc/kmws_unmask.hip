@@ -187,14 +187,13 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
 // blocks past k * (nfull / k) take the remaining tiles in order).  With c > 0
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
-// its own runs), inside w windows far apart (consecutive blocks of a residue
-// alternate between the windows).
+// its own runs).
 template <int V>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w)
+                                                              uint32_t k, uint32_t c, uint32_t b0)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -205,13 +204,11 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     if (c == 0) {  // k equal parts
         const uint32_t q = nfull / k;
         if (b < q * k) tile = (b % k) * q + b / k;
-    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k, in w windows
+    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k
         const uint64_t run = (uint64_t)k * c;
-        const uint64_t per = (uint64_t)nfull / w / run * run;  // tiles per window
-        if (b < per * w) {
+        if (b < nfull / run * run) {
             const uint32_t x = b % k, i = b / k;
-            const uint32_t j = i % w, i2 = i / w;  // window, position in the residue's stream
-            tile = (uint32_t)(j * per) + (i2 / c) * (uint32_t)run + x * c + i2 % c;
+            tile = (i / c) * (uint32_t)run + x * c + i % c;
         }
     }
     const uint64_t lo = (uint64_t)tile * Cfg::kTile;
@@ -290,76 +287,6 @@ __global__ void __launch_bounds__(kBlock) unmask_pipe_kernel(uint8_t* __restrict
         const bool a = step(va, vb);
         const bool b = step(vb, va);
         if (!(a & b)) break;
-    }
-}
-
-// Work queue over the full tiles: a grid of about one resident block per slot
-// takes chunks of `chunk` tiles from a counter in the workspace head (pad[0]),
-// so every block streams until the queue is empty and no block generation is
-// left half full at the end (the grid-stride schedules above run 16-32 block
-// generations; a grid that is not a multiple of the resident count leaves
-// the last one part-empty).  Thread 0 takes the NEXT chunk while the current
-// one streams (one device-scope atomic per chunk) and publishes it through LDS
-// at the chunk boundary.  The last block out resets the counters (pad[0..1]),
-// so the workspace is left as the plan wrote it.
-template <int V>
-__global__ void __launch_bounds__(kBlock) unmask_queue_kernel(uint8_t* __restrict__ base,
-                                                              const kmws_desc* __restrict__ d, uint32_t n,
-                                                              const uint32_t* __restrict__ map,
-                                                              WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t chunk)
-{
-    using Cfg = UnmaskCfg<V>;
-    __shared__ uint64_t s_off[Cfg::kCap];
-    __shared__ uint64_t s_end[Cfg::kCap];
-    __shared__ uint32_t s_key[Cfg::kCap];
-    __shared__ uint32_t s_grab;
-    uint32_t* q = &head->pad[0];
-    const bool ok = head->status == 0;
-    const bool lead = threadIdx.x == 0;
-    if (lead) s_grab = atomicAdd(q, chunk);
-    __syncthreads();
-    uint32_t t = s_grab;
-    // Thread 0 takes the next chunk.  Every lane of wave 0 runs the atomic (the
-    // others add 0): a lane-0-only atomic ends a divergent branch, and the
-    // compiler waits for ALL outstanding loads at its join.
-    const bool w0 = threadIdx.x < 64;
-    const uint32_t add = lead ? chunk : 0u;
-    uint32_t next = w0 ? atomicAdd(q, add) : 0u;
-    if (t < nfull) {
-        uint32_t cend = t + chunk < nfull ? t + chunk : nfull;
-        u32x4 va[V], vb[V];
-        load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, va);
-        auto step = [&](const u32x4(&vc)[V], u32x4(&vn)[V]) __attribute__((always_inline)) {
-            uint32_t tn = t + 1;
-            if (tn >= cend) {  // block-uniform: chunk boundary
-                __syncthreads();  // every lane has read the previous s_grab
-                if (lead) s_grab = next;
-                __syncthreads();
-                tn = s_grab;
-                cend = tn + chunk < nfull ? tn + chunk : nfull;
-                if (w0) next = atomicAdd(q, tn < nfull ? add : 0u);
-            }
-            const bool more = tn < nfull;
-            load_tile<V, true>(base, (uint64_t)(more ? tn : t) * Cfg::kTile, 0, vn);
-            __builtin_amdgcn_sched_barrier(0);
-            const uint64_t lo = (uint64_t)t * Cfg::kTile;
-            finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, t, ok, vc, s_off, s_end, s_key);
-            __builtin_amdgcn_sched_barrier(0);
-            t = tn;
-            return more;
-        };
-        for (;;) {
-            if (!step(va, vb)) break;
-            if (!step(vb, va)) break;
-        }
-    }
-    if (lead) {
-        __threadfence();
-        if (atomicAdd(&head->pad[1], 1u) == gridDim.x - 1) {  // every block is past its last take
-            atomicExch(&head->pad[0], 0u);
-            atomicExch(&head->pad[1], 0u);
-        }
     }
 }
 
@@ -601,38 +528,9 @@ static uint32_t resident_blocks(const void* kernel)
 }
 
 template <int V>
-static kmws_status launch_apply_queue(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                      const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t per_slot,
-                                      uint32_t chunk)
-{
-    using Cfg = UnmaskCfg<V>;
-    uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
-    if (st != KMWS_OK) return st;
-    if (n == 0 || span == 0) return KMWS_OK;
-    // the kernel only borrows the head's queue words and zeroes them again
-    WsHead* head = const_cast<WsHead*>(static_cast<const WsHead*>(workspace));
-    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
-    const uint64_t nfull = span / Cfg::kTile;
-    if (nfull > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
-    if (nfull) {
-        const uint32_t r = resident_blocks(reinterpret_cast<const void*>(unmask_queue_kernel<V>));
-        if (r == 0) return KMWS_ERR_FAILED;
-        const uint64_t want = (uint64_t)r * per_slot;
-        const uint32_t g = (uint32_t)(want < nfull ? want : nfull);
-        hipLaunchKernelGGL(unmask_queue_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
-                           (uint32_t)nfull, chunk);
-    }
-    if (ntiles > nfull)  // the partial last tile
-        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
-                           (uint32_t)nfull);
-    return hip_status(hipGetLastError());
-}
-
-template <int V>
 static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
-                                      uint32_t c = 0, uint32_t w = 1)
+                                      uint32_t c = 0)
 {
     using Cfg = UnmaskCfg<V>;
     uint64_t ntiles = 0;
@@ -648,7 +546,7 @@ static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_d
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
         hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
-                           head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+                           head, (uint32_t)nfull, k, c, (uint32_t)b0);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
@@ -830,26 +728,6 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         static const uint32_t grids[] = {16384u, 32768u, 65536u};
         return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, grids[variant - 10]);
     }
-    case 13:
-    case 14:
-    case 15:
-    case 16: {  // 16 KiB tiles, work queue: chunk 1 / 4 / 16 tiles on the resident grid, chunk 4 on twice it
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t chunks[] = {1u, 4u, 16u, 4u};
-        return launch_apply_queue<4>(base, span, descs, n, workspace, workspace_bytes, s, variant == 16 ? 2u : 1u,
-                                     chunks[variant - 13]);
-    }
-    case 17:
-    case 18:
-    case 19:
-    case 20: {  // 16 KiB tiles, pipelined grid of 1 / 2 / 4 / 8 x the resident blocks
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        const uint32_t r = resident_blocks(reinterpret_cast<const void*>(unmask_pipe_kernel<4>));
-        if (r == 0) return KMWS_ERR_FAILED;
-        return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, r << (variant - 17));
-    }
     case 21:
     case 22:
     case 23:
@@ -882,26 +760,6 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
         if (st != KMWS_OK) return st;
         return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, variant == 34 ? 2u : 8u);
-    }
-    case 40:
-    case 41:
-    case 42:
-    case 43:
-    case 44:
-    case 45:
-    case 46:
-    case 47: {  // runs of c tiles per XCD residue, in w far-apart windows: (c, w) below
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t cw[][2] = {{16, 2}, {16, 4}, {16, 8}, {128, 2}, {128, 8}, {4, 8}, {1, 8}, {16, 16}};
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, cw[variant - 40][0],
-                                     cw[variant - 40][1]);
-    }
-    case 48:
-    case 49: {  // 32 KiB tiles, runs of 8 / 16 tiles per XCD residue
-        kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, 8u, variant == 48 ? 8u : 16u);
     }
     default:
         if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)

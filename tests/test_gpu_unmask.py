@@ -93,7 +93,7 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 65537])
+@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 66, 65537, 2097152])
 def test_unmask_parity(torch_dev, kind, variant):
     rng = np.random.default_rng(abs(hash((kind, variant))) % 2**32)
     buf, descs = layout(kind, rng)
@@ -206,7 +206,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
 
 
 @pytest.mark.parametrize("frame_len", [65536, 65531, 3000])
-@pytest.mark.parametrize("variant", [None, 4, 10, 13, 14, 15, 16, 17, 20, 21, 24, 25, 27, 2097152])
+@pytest.mark.parametrize("variant", [None, 4, 10, 21, 23, 24, 27, 2097152])
 def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len):
     """512 MiB arena (32 K tiles: several tiles and queue chunks per block of the
     persistent / queue schedules), payload generated on the device, every byte
