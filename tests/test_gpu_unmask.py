@@ -205,17 +205,19 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     assert st == 0 and np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("frame_len", [65536, 65531, 3000])
-@pytest.mark.parametrize("variant", [None, 4, 10, 21, 23, 24, 27, 2097152])
-def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len):
-    """512 MiB arena (32 K tiles: several tiles and queue chunks per block of the
-    persistent / queue schedules), payload generated on the device, every byte
-    checked on the device against the generator (payload ^ key inside frames,
-    untouched gaps).  Applied twice more on the same plan (XOR twice = identity)
-    with the queue schedules, whose counters must be back at zero."""
+@pytest.mark.parametrize("frame_len,tail", [(65536, 0), (65531, 0), (3000, 0), (65531, 7 * 16384 + 100)])
+@pytest.mark.parametrize("variant", [None, 4, 10, 21, 23, 24, 25, 27, 29, 30, 2097152, 65537])
+def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len, tail):
+    """512 MiB arena (32 K tiles: many tiles per block of the persistent
+    schedules, whole runs and parts of the XCD-run and split mappings), plus a
+    tail that is not a whole number of runs / parts (and a partial last tile):
+    payload generated on the device, every byte checked on the device against
+    the generator (payload ^ key inside frames, untouched gaps).  Applied three
+    times (odd), so a schedule that skipped or doubled a tile shows up."""
     torch = torch_dev
     from kuma_amd import kmws
-    stride, span = 65536 if frame_len > 4096 else 4096, 512 << 20
+    stride = 65536 if frame_len > 4096 else 4096
+    span = (512 << 20) + tail
     n = span // stride
     base = torch.empty(span, dtype=torch.uint8, device="cuda")
     descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
