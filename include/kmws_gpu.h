@@ -186,9 +186,10 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * them with events on `stream` (synchronizes) and makes the fastest the
  * current device's schedule for kmws_unmask_apply / kmws_unmask_batch.
  * Returns the chosen schedule or a negative status, one block per 16 KiB tile:
- * runs of 16 tiles per XCD (0, the default), in order (1), tiles dealt over 2
- * (2) or 8 (3) far-apart parts of the span; >= 64: a persistent grid of that
- * many blocks (+1: the pipelined grid).  kmws_unmask_schedule() reports the current one. */
+ * the XCDs in 2 groups, each dealing runs of 16 tiles inside its own half of
+ * the span (0, the default), in order (1), tiles dealt over 2 (2) or 8 (3)
+ * far-apart parts of the span, runs of 16 tiles per XCD (4); >= 64: a
+ * persistent grid of that many blocks (+1: the pipelined grid).  kmws_unmask_schedule() reports the current one. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
 int kmws_unmask_schedule(void);
@@ -202,8 +203,10 @@ int kmws_unmask_resident_blocks(void);
  * or 8 (9) waves per SIMD; pipelined persistent grid of 16 K (10), 32 K (11) or
  * 64 K (12) blocks; one block per 16 KiB tile dealt over 2, 4, 8, 16 (21-24) or
  * 3, 6, 12, 32 (30-33) parts of the span, or in runs of 4, 8, 16, 32, 128 tiles
- * over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8 parts (34, 35); any value
- * >= 64: a schedule code as kmws_unmask_schedule() returns. */
+ * over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8 parts (34, 35); runs of 16
+ * tiles per XCD with the XCDs in 2 / 4 / 8 groups, each group in its own part of
+ * the span (36-38); any value >= 64: a schedule code as kmws_unmask_schedule()
+ * returns. */
 kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       void* workspace, size_t workspace_bytes, void* stream, int variant);
 

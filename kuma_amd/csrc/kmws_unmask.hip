@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t k, uint32_t c, uint32_t b0)
+                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -204,11 +204,20 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     if (c == 0) {  // k equal parts
         const uint32_t q = nfull / k;
         if (b < q * k) tile = (b % k) * q + b / k;
-    } else {  // runs of c tiles dealt round-robin over the k residues of b mod k
+    } else if (w <= 1) {  // runs of c tiles dealt round-robin over the k residues of b mod k
         const uint64_t run = (uint64_t)k * c;
         if (b < nfull / run * run) {
             const uint32_t x = b % k, i = b / k;
             tile = (i / c) * (uint32_t)run + x * c + i % c;
+        }
+    } else {  // residues split into w groups, each group's runs inside its own far-apart window
+        const uint32_t kg = k / w;                      // residues per group
+        const uint64_t run = (uint64_t)kg * c;          // tiles per round of a group's runs
+        const uint64_t per = (uint64_t)nfull / w / run * run;
+        if (b < per * w) {
+            const uint32_t x = b % k, i = b / k;
+            const uint32_t g = x % w, xi = x / w;
+            tile = (uint32_t)(g * per) + (i / c) * (uint32_t)run + xi * c + i % c;
         }
     }
     const uint64_t lo = (uint64_t)tile * Cfg::kTile;
@@ -410,8 +419,10 @@ constexpr int kUnmaskV = 4;
 // flight are decides the rate: the in-order grid streams one 16 MiB window
 // (74.5-75 % of HBM peak everywhere); dealing blocks over 8 parts of the span
 // streams 8 windows far apart (82-83 % on some 64 GiB placements in HBM, 76 %
-// on others); runs of 16 tiles per XCD hold 78-79 % on every placement and 82 %
-// on 4 KiB frames (profiles/r01f_unmask_placement.txt).  Default: XCD runs;
+// on others); runs of 16 tiles per XCD hold 78-79 % on every placement; two
+// groups of 4 XCDs, each with runs of 16 in its own half of the span, match
+// the better of the two on every placement measured and lead on 4 KiB frames
+// (82 %) (profiles/r01f_unmask_placement.txt).  Default: the grouped runs;
 // kmws_unmask_autotune picks per device on the caller's batch.
 constexpr int kMaxDevices = 64;
 static uint32_t g_schedule[kMaxDevices];
@@ -530,7 +541,7 @@ static uint32_t resident_blocks(const void* kernel)
 template <int V>
 static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
-                                      uint32_t c = 0)
+                                      uint32_t c = 0, uint32_t w = 1)
 {
     using Cfg = UnmaskCfg<V>;
     uint64_t ntiles = 0;
@@ -546,7 +557,7 @@ static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_d
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
         hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
-                           head, (uint32_t)nfull, k, c, (uint32_t)b0);
+                           head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
@@ -563,14 +574,17 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
 }
 
-// Schedule code, one block per 16 KiB tile: runs of 16 tiles per XCD (0, the
-// default), in order (1), tiles dealt over 2 parts of the span (2) or over 8
-// parts (3); codes >= 64: a persistent grid of that many blocks, grid-stride
-// (even) or software-pipelined (odd, grid = code - 1).
+// Schedule code, one block per 16 KiB tile: the XCDs in 2 groups of 4, each
+// group dealing runs of 16 tiles to its XCDs inside its own half of the span
+// (0, the default), in order (1), tiles dealt over 2 parts of the span (2) or
+// over 8 parts (3), runs of 16 tiles per XCD in one window (4); codes >= 64: a
+// persistent grid of that many blocks, grid-stride (even) or software-pipelined
+// (odd, grid = code - 1).
 static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                    const void* workspace, size_t ws_bytes, hipStream_t s)
 {
-    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
+    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u, 2u);
+    if (code == 4) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
     if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
     if (code == 2) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 2u);
     if (code == 3) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
@@ -655,9 +669,10 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     hipStream_t s = static_cast<hipStream_t>(stream);
     kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    // XCD runs, 8 parts, 2 parts, in order: which wins depends on where the batch
-    // lies in HBM and on its frame layout (profiles/r01f_unmask_placement.txt)
-    static const uint32_t cand[] = {0u, 3u, 2u, 1u};
+    // grouped XCD runs, 8 parts, XCD runs, 2 parts, in order: which wins depends on
+    // where the batch lies in HBM and on its frame layout
+    // (profiles/r01f_unmask_placement.txt)
+    static const uint32_t cand[] = {0u, 3u, 4u, 2u, 1u};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {
@@ -760,6 +775,14 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
         if (st != KMWS_OK) return st;
         return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, variant == 34 ? 2u : 8u);
+    }
+    case 36:
+    case 37:
+    case 38: {  // XCD runs of 16 tiles, the 8 residues in 2 / 4 / 8 groups, each group in its own window
+        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, 16u,
+                                     2u << (variant - 36));
     }
     default:
         if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)

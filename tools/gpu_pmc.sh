@@ -18,6 +18,9 @@ python3 tools/pmc_traffic.py "$OUT/split_fetch" "$OUT/split_write" unmask_split_
 pass split8_fetch FETCH_SIZE "--variant 23" &&
 pass split8_write WRITE_SIZE "--variant 23" &&
 python3 tools/pmc_traffic.py "$OUT/split8_fetch" "$OUT/split8_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split8.json" 3 &&
+pass runs_fetch FETCH_SIZE "--variant 27" &&
+pass runs_write WRITE_SIZE "--variant 27" &&
+python3 tools/pmc_traffic.py "$OUT/runs_fetch" "$OUT/runs_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_runs.json" 4 &&
 pass tiles_fetch FETCH_SIZE "--variant 0" &&
 pass tiles_write WRITE_SIZE "--variant 0" &&
 python3 tools/pmc_traffic.py "$OUT/tiles_fetch" "$OUT/tiles_write" unmask_tiles_kernel 1048576 65536 "$OUT/traffic.json" &&
