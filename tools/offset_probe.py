@@ -19,7 +19,7 @@ def main():
     n, L = 1 << 20, 65536
     span = n * L
     a = kmws.Arena(total << 30)
-    print(json.dumps({"contiguous": a.contiguous, "total_GiB": total}), flush=True)
+    print(json.dumps({"contiguous": a.contiguous, "total_GiB": total, "va_GiB": a.tensor.data_ptr() / 2**30}), flush=True)
     kmws.fill_synthetic(a.tensor, 5)
     descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
     kmws.fill_uniform_descs(descs, L, L, 3)
