@@ -9,6 +9,11 @@ place.  Payload and keys are synthetic (counter-based splitmix64, generated
 on device, untimed).  With --gpus N (torchrun, one rank per GPU) every rank
 unmasks its own batch: a plain per-GPU frame partition (weak scaling), no
 data-path collective; the barrier and the max-over-ranks timing use RCCL.
+--job-frames J instead fixes the job (strong scaling, BASELINE configs[4]:
+10,485,760 frames over 1/2/4/8 GPUs): a rank whose shard exceeds one
+resident batch (--max-batch-frames, 80 GiB) runs it as sub-batches, each
+generated on device untimed and timed like one batch; the step time is the
+sum over sub-batches.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the formulas.
 """
@@ -34,6 +39,11 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
+    p.add_argument("--job-frames", type=int, default=0,
+                   help="strong scaling: a fixed job of this many frames split over the ranks (configs[4]: 10485760); "
+                        "0 = weak scaling, --frames per GPU")
+    p.add_argument("--max-batch-frames", type=int, default=1310720,
+                   help="largest resident batch per GPU (80 GiB of 64 KiB frames); larger shards run as sub-batches")
     p.add_argument("--frame-len", type=int, default=65536)
     p.add_argument("--variant", type=int, default=-1, help="tile variant (-1 = product default)")
     p.add_argument("--seed", type=int, default=0x6B756D61)
@@ -198,84 +208,106 @@ def main():
         raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
 
     from kuma_amd import shard
-    n, L = a.frames, a.frame_len
+    L = a.frame_len
+    # The job: world x frames (weak scaling, default) or --job-frames J split over
+    # the ranks (strong scaling, BASELINE configs[4]: 10 M frames on 1..8 GPUs).
+    # Rank g owns global frames [lo, hi) (kuma_amd/shard.py); payload and keys are
+    # generated from global positions, so the shards are slices of one big job.
+    job = a.job_frames if a.job_frames else a.frames * world
+    g_lo, g_hi = shard.uniform_range(job, rank, world)
+    # A shard larger than one resident batch runs as `nb` sub-batches (same count
+    # on every rank), each generated on device untimed, then timed like one batch.
+    max_shard = -(-job // world)
+    nb = -(-max_shard // a.max_batch_frames)
+    n = -(-max_shard // nb)  # frames per resident batch (the last one may be shorter)
     span = n * L
-    # Weak scaling: the job is world x n frames; rank g owns global frames
-    # [g*n, (g+1)*n) (kuma_amd/shard.py).  Data and keys are generated from
-    # global positions, so the shards are slices of one big batch.
-    g_lo, g_hi = shard.uniform_range(n * world, rank, world)
-    assert g_hi - g_lo == n
-    seed = a.seed + (g_lo * L >> 3)
-    key_seed = (a.seed ^ 0x5EED) + g_lo
     descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span), device=dev)
-    kmws.fill_uniform_descs(descs, L, L, key_seed)
+    kmws.fill_uniform_descs(descs, L, L, (a.seed ^ 0x5EED) + g_lo)
     arena, placement = None, {"kind": "plain torch.empty"}
     if a.placement == "probe":
-        arena, base, placement = place_batch(kmws, torch, dev, span, descs, ws, a.placement_slack_gib << 30)
+        arena, base_all, placement = place_batch(kmws, torch, dev, span, descs, ws, a.placement_slack_gib << 30)
     if arena is None:
-        base = torch.empty(span, dtype=torch.uint8, device=dev)
-    kmws.fill_synthetic(base, seed)
-    torch.cuda.synchronize()
+        base_all = torch.empty(span, dtype=torch.uint8, device=dev)
 
     variant = None if a.variant < 0 else a.variant
     stream = torch.cuda.current_stream()
-
-    def step(ev0=None, ev1=None):
-        if variant is None:
-            kmws.unmask_plan(descs, ws, span)
-            if ev0 is not None:
-                ev0.record(stream)
-            kmws.unmask_apply(base, descs, ws, span)
-            if ev1 is not None:
-                ev1.record(stream)
-        else:
-            if ev0 is not None:
-                ev0.record(stream)
-            kmws.unmask_batch(base, descs, ws, span, variant=variant)
-            if ev1 is not None:
-                ev1.record(stream)
-
     schedule = 0
-    if variant is None and not a.no_autotune:
-        # untimed, payload unchanged: picks this box's faster unmask schedule
-        schedule = kmws.unmask_autotune(base, descs, ws, span)
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(*evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    elapsed, ev_ms, launches, alg_total, mismatches, st, done = 0.0, 0.0, 0, 0, 0, 0, 0
+    for j in range(nb):
+        b_lo = min(g_lo + j * n, g_hi)
+        bn = min(n, g_hi - b_lo)
+        bspan = bn * L
+        base, bdescs = base_all[:bspan], descs[:bn]
+        seed = a.seed + (b_lo * L >> 3)
+        if bn:
+            kmws.fill_uniform_descs(bdescs, L, L, (a.seed ^ 0x5EED) + b_lo)
+            kmws.fill_synthetic(base, seed)
+        torch.cuda.synchronize()
+
+        def step(ev0=None, ev1=None):
+            if bn == 0:
+                return
+            if variant is None:
+                kmws.unmask_plan(bdescs, ws, bspan)
+                if ev0 is not None:
+                    ev0.record(stream)
+                kmws.unmask_apply(base, bdescs, ws, bspan)
+                if ev1 is not None:
+                    ev1.record(stream)
+            else:
+                if ev0 is not None:
+                    ev0.record(stream)
+                kmws.unmask_batch(base, bdescs, ws, bspan, variant=variant)
+                if ev1 is not None:
+                    ev1.record(stream)
+
+        if j == 0 and bn and variant is None and not a.no_autotune:
+            # untimed, payload unchanged: picks this box's faster unmask schedule
+            schedule = kmws.unmask_autotune(base, bdescs, ws, bspan)
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(*evs[i])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed += time.perf_counter() - t0
+        if bn:
+            ev_ms += sum(e0.elapsed_time(e1) for e0, e1 in evs)
+            launches += a.steps
+            alg_total += a.steps * bn * (2 * L + DESC_BYTES)
+        done += bn
+        st |= ws.status()
+        if not a.no_verify and bn:
+            if (a.warmup + a.steps) % 2 == 0:  # XOR twice is the identity: bring the batch to the unmasked state
+                kmws.unmask_batch(base, bdescs, ws, bspan)
+            mismatches += kmws.check_unmasked(base, seed, bdescs)
+    assert done == g_hi - g_lo
+    # average unmask-kernel launch: duration and algorithmic bytes (every batch is
+    # full, n frames, when nb divides the shard)
+    kern_ms = ev_ms / max(launches, 1)
+    alg_bytes = alg_total // max(launches, 1)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+    if a.no_verify:
+        mismatches = None
+    elif world > 1:
+        t = torch.tensor([mismatches], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(t)
+        mismatches = int(t[0])
 
-    st = ws.status()
-    mismatches = None
-    if not a.no_verify:
-        applied = a.warmup + a.steps
-        if applied % 2 == 0:  # XOR twice is the identity: bring the arena to the unmasked state
-            kmws.unmask_batch(base, descs, ws, span)
-        mismatches = kmws.check_unmasked(base, seed, descs)
-        if world > 1:
-            t = torch.tensor([mismatches], dtype=torch.int64, device=coll_dev)
-            dist.all_reduce(t)
-            mismatches = int(t[0])
-
-    ms_per_step = elapsed * 1e3 / a.steps
-    total_payload = world * span
-    value = shard.aggregate_rate([span * a.steps] * world, [elapsed] * world) / 2**30
-    alg_bytes = n * (2 * L + DESC_BYTES)
+    ms_per_step = elapsed * 1e3 / a.steps  # one step = one pass over the rank's shard
+    total_payload = job * L
+    value = total_payload * a.steps / elapsed / 2**30  # = shard.aggregate_rate over ranks (elapsed = max)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     kernel = schedule_kernel(schedule) if variant is None else f"kmws_unmask_batch_variant({variant})"
     traffic = traffic_from_profile(n, L, kernel, schedule if variant is None else None)
@@ -289,11 +321,14 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": "strong" if a.job_frames else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (device-generated splitmix64 payload, per-frame random keys)",
-            "config": {"workload": "cfg2: 1 GPU device-resident in-place unmask of masked binary frames "
+            "config": {"workload": ("cfg5: fixed job of %d frames split over the GPUs (per-GPU frame partition), "
+                                    "device-resident in-place unmask" % job) if a.job_frames else
+                                   "cfg2: 1 GPU device-resident in-place unmask of masked binary frames "
                                    "(aligned arena); N GPUs = per-GPU frame partition",
-                       "frames_per_gpu": n, "frame_len": L, "total_frames": n * world,
+                       "frames_per_gpu": g_hi - g_lo, "frame_len": L, "total_frames": job,
+                       "resident_batch_frames": n, "sub_batches": nb,
                        "layout": "aligned arena, frame i at i*frame_len",
                        "parallelism": f"frame-partition x{world} (no collective)",
                        "tile_variant": "default" if variant is None else variant,
