@@ -215,11 +215,10 @@ def main():
     # generated from global positions, so the shards are slices of one big job.
     job = a.job_frames if a.job_frames else a.frames * world
     g_lo, g_hi = shard.uniform_range(job, rank, world)
-    # A shard larger than one resident batch runs as `nb` sub-batches (same count
-    # on every rank), each generated on device untimed, then timed like one batch.
-    max_shard = -(-job // world)
-    nb = -(-max_shard // a.max_batch_frames)
-    n = -(-max_shard // nb)  # frames per resident batch (the last one may be shorter)
+    # A shard larger than one resident batch runs as sub-batches (same count on
+    # every rank), each generated on device untimed, then timed like one batch.
+    n, batches = shard.sub_batches(job, rank, world, a.max_batch_frames)
+    nb = len(batches)
     span = n * L
     descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span), device=dev)
@@ -234,9 +233,8 @@ def main():
     stream = torch.cuda.current_stream()
     schedule = 0
     elapsed, ev_ms, launches, alg_total, mismatches, st, done = 0.0, 0.0, 0, 0, 0, 0, 0
-    for j in range(nb):
-        b_lo = min(g_lo + j * n, g_hi)
-        bn = min(n, g_hi - b_lo)
+    for j, (b_lo, b_hi) in enumerate(batches):
+        bn = b_hi - b_lo
         bspan = bn * L
         base, bdescs = base_all[:bspan], descs[:bn]
         seed = a.seed + (b_lo * L >> 3)

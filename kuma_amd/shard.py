@@ -21,6 +21,23 @@ def uniform_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return (rank * n) // world, ((rank + 1) * n) // world
 
 
+def sub_batches(job: int, rank: int, world: int, max_batch: int) -> Tuple[int, List[Tuple[int, int]]]:
+    """Resident sub-batches of rank `rank`'s shard of a `job`-frame job.
+
+    Every rank gets the same number of sub-batches (so the harness barriers
+    pair up), each at most `max_batch` frames: returns (frames per full batch,
+    [(lo, hi) global frame ranges]), covering the shard in order.  A rank with a
+    shorter shard may have a short or empty last sub-batch.
+    """
+    if max_batch < 1:
+        raise ValueError("max_batch must be >= 1")
+    lo, hi = uniform_range(job, rank, world)
+    max_shard = -(-job // world)
+    nb = max(1, -(-max_shard // max_batch))
+    n = -(-max_shard // nb)
+    return n, [(min(lo + j * n, hi), min(lo + (j + 1) * n, hi)) for j in range(nb)]
+
+
 def byte_balanced_ranges(lens: Sequence[int], world: int) -> List[Tuple[int, int]]:
     """Contiguous frame ranges with near-equal payload bytes per rank.
 

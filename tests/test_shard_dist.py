@@ -23,6 +23,25 @@ def test_uniform_ranges_cover():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_sub_batches_cover_and_pair_up():
+    # BASELINE configs[4]: 10 M frames over 1/2/4/8 GPUs, 80 GiB resident batches
+    for job, mb in ((10485760, 1310720), (1 << 20, 1310720), (1 << 20, 262144), (7, 2), (0, 5), (13, 100)):
+        for world in (1, 2, 3, 4, 8):
+            counts = set()
+            for g in range(world):
+                n, bs = shard.sub_batches(job, g, world, mb)
+                lo, hi = shard.uniform_range(job, g, world)
+                counts.add(len(bs))
+                assert n <= max(mb, 1)
+                assert bs[0][0] == lo and bs[-1][1] == hi
+                assert all(b[1] == c[0] for b, c in zip(bs, bs[1:]))
+                assert all(0 <= b - a <= n for a, b in bs)
+            assert len(counts) == 1  # same sub-batch count on every rank
+    n, bs = shard.sub_batches(10485760, 0, 1, 1310720)
+    assert n == 1310720 and len(bs) == 8
+    assert shard.sub_batches(10485760, 7, 8, 1310720) == (1310720, [(9175040, 10485760)])
+
+
 def test_byte_balanced_ranges():
     rng = np.random.default_rng(0)
     lens = 128 * 2 ** rng.integers(0, 14, size=5000)
