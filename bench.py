@@ -143,10 +143,9 @@ def traffic_from_profile(frames: int, frame_len: int, kernel: str, schedule=None
 
 
 PLACEMENT_STEP = 16 << 30
-PROBE_VARIANT = 23  # split 8: the schedule whose rate depends most on where the batch lies
 
 
-def place_batch(kmws, torch, dev, span, descs, ws, slack):
+def place_batch(kmws, torch, dev, span, slack):
     """Carves the batch out of one physically contiguous arena of span + slack
     bytes, at the offset (multiples of 16 GiB) where two in-place split-8 unmask
     passes (payload unchanged) run fastest.  The rate of the split schedules
@@ -162,25 +161,11 @@ def place_batch(kmws, torch, dev, span, descs, ws, slack):
         arena = kmws.Arena(span + slack, device=dev.index)
     except RuntimeError as e:
         return None, None, {"kind": "plain torch.empty", "why": str(e)}
-    alg = descs.shape[0] * (2 * (span // descs.shape[0]) + DESC_BYTES)
-    s = torch.cuda.current_stream()
-    probe = {}
-    for off in range(0, slack + 1, PLACEMENT_STEP):
-        view = arena.tensor[off:off + span]
-        best = None
-        for _ in range(2):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(2):  # XOR twice: payload unchanged
-                kmws.unmask_batch(view, descs, ws, span, variant=PROBE_VARIANT)
-            e1.record(s)
-            e1.synchronize()
-            ms = e0.elapsed_time(e1) / 2
-            best = ms if best is None else min(best, ms)
-        probe[off >> 30] = round(alg / (best * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    pick = max(probe, key=probe.get)
-    rec = {"kind": "offset in a contiguous arena, picked by a timed split-8 probe", "arena_GiB": (span + slack) >> 30,
-           "contiguous": arena.contiguous, "offset_GiB": pick, "probe_frac_by_offset_GiB": probe}
+    off, probe = kmws.arena_place(arena, span, PLACEMENT_STEP)  # kmws_arena_place: timed split-8 passes
+    pick = off >> 30
+    rec = {"kind": "offset in a contiguous arena, picked by kmws_arena_place (timed split-8 probe)",
+           "arena_GiB": (span + slack) >> 30, "contiguous": arena.contiguous, "offset_GiB": pick,
+           "probe_frac_by_offset_GiB": {o >> 30: v for o, v in probe.items()}}
     return arena, arena.tensor[pick << 30:(pick << 30) + span], rec
 
 
@@ -225,7 +210,7 @@ def main():
     kmws.fill_uniform_descs(descs, L, L, (a.seed ^ 0x5EED) + g_lo)
     arena, placement = None, {"kind": "plain torch.empty"}
     if a.placement == "probe":
-        arena, base_all, placement = place_batch(kmws, torch, dev, span, descs, ws, a.placement_slack_gib << 30)
+        arena, base_all, placement = place_batch(kmws, torch, dev, span, a.placement_slack_gib << 30)
     if arena is None:
         base_all = torch.empty(span, dtype=torch.uint8, device=dev)
 

@@ -299,6 +299,18 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
 void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous);
 void  kmws_arena_free(void* p, int device);
 
+/* Placement probe for a long-lived batch region inside an arena: times an
+ * in-place split-8 unmask of `span` bytes (uniform 64 KiB probe frames, applied
+ * twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step, ...
+ * (offset + span <= arena_bytes) and returns the byte offset of the fastest,
+ * or a negative kmws_status.  The split schedules run 76 % or 82-83 % of HBM
+ * peak depending on where the batch lies in physical HBM, which the kernel
+ * cannot see (DESIGN.md sec.4 "Placement").  frac_out (optional, max_out
+ * entries) receives each offset's rate as a fraction of 8 TB/s.  A setup call:
+ * allocates its probe descriptors and workspace, synchronizes the stream. */
+int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, uint64_t step, void* stream,
+                         float* frac_out, uint32_t max_out);
+
 /* ---- synthetic data + checks (bench / test support, device side) ---- */
 
 /* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */

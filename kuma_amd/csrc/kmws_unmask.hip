@@ -835,6 +835,69 @@ void kmws_arena_free(void* p, int device)
     if (device != prev) (void)hipSetDevice(prev);
 }
 
+int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, uint64_t step, void* stream,
+                         float* frac_out, uint32_t max_out)
+{
+    // Offsets 0, step, 2 step, ... with offset + span <= arena_bytes.  The probe
+    // batch: uniform 64 KiB frames over the span (contents are whatever the arena
+    // holds; XOR applied twice leaves them unchanged), split-8 schedule (code 3).
+    constexpr uint64_t kFrame = 65536;
+    if (!arena || span == 0 || span > arena_bytes || step == 0 || (step & 15u) ||
+        (reinterpret_cast<uintptr_t>(arena) & 15u) || span / kFrame > 0xFFFFFFFFull)
+        return KMWS_ERR_INVALID_PARAM;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t n = (uint32_t)((span + kFrame - 1) / kFrame);
+    const size_t ws_bytes = kmws_unmask_workspace_size(span);
+    kmws_desc* d = nullptr;
+    void* ws = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int64_t result = KMWS_ERR_FAILED;
+    if (hipMalloc(reinterpret_cast<void**>(&d), (size_t)n * sizeof(kmws_desc)) != hipSuccess ||
+        hipMalloc(&ws, ws_bytes) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess) {
+        (void)hipGetLastError();
+    } else {
+        hipLaunchKernelGGL(uniform_descs_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, d, n, kFrame,
+                           (uint32_t)kFrame, 0x706c6163ull);
+        // the last frame ends at the span (uniform_descs gives every frame kFrame bytes)
+        const uint32_t last_len = (uint32_t)(span - (uint64_t)(n - 1) * kFrame);
+        kmws_status st = hip_status(hipMemcpyAsync(&d[n - 1].len, &last_len, sizeof(last_len),
+                                                   hipMemcpyHostToDevice, s));
+        if (st == KMWS_OK) st = hip_status(hipStreamSynchronize(s));
+        float best = 1e30f;
+        uint64_t pick = 0;
+        uint32_t k = 0;
+        for (uint64_t off = 0; st == KMWS_OK && off + span <= arena_bytes; off += step, ++k) {
+            float t = 1e30f;
+            for (int rep = 0; rep < 2 && st == KMWS_OK; ++rep) {  // min of two pairs
+                st = launch_plan<kUnmaskV>(span, d, n, ws, ws_bytes, s);
+                if (st == KMWS_OK) st = hip_status(hipEventRecord(e0, s));
+                for (int i = 0; i < 2 && st == KMWS_OK; ++i)
+                    st = launch_schedule(3u, arena + off, span, d, n, ws, ws_bytes, s);
+                if (st == KMWS_OK) st = hip_status(hipEventRecord(e1, s));
+                if (st == KMWS_OK) st = hip_status(hipEventSynchronize(e1));
+                float ms = 0;
+                if (st == KMWS_OK && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < t) t = ms;
+            }
+            if (st != KMWS_OK) break;
+            // fraction of the 8 TB/s HBM peak: 2 passes x (2 span + 16 n) bytes
+            if (frac_out && k < max_out) frac_out[k] = (float)(2.0 * (2.0 * span + 16.0 * n) / (t * 1e-3) / 8e12);
+            if (t < best) {
+                best = t;
+                pick = off;
+            }
+        }
+        uint32_t status = 0;
+        if (st == KMWS_OK) st = hip_status(hipMemcpy(&status, ws, sizeof(status), hipMemcpyDeviceToHost));
+        result = st != KMWS_OK ? (int64_t)st : (status != 0 ? (int64_t)KMWS_ERR_FAILED : (int64_t)pick);
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (ws) (void)hipFree(ws);
+    if (d) (void)hipFree(d);
+    return result;
+}
+
 kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream)
 {
     if (!base && bytes) return KMWS_ERR_INVALID_PARAM;

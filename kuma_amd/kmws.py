@@ -37,7 +37,7 @@ EXPORTS = [
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
-    "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free",
+    "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place",
 ]
 
 
@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
         "kmws_arena_alloc": (vp, [u64, i32, C.POINTER(C.c_int)]),
         "kmws_arena_free": (None, [vp, i32]),
+        "kmws_arena_place": (C.c_int64, [u8p, u64, u64, u64, vp, C.POINTER(C.c_float), u32]),
         "kmws_fill_uniform_descs": (i32, [vp, u32, u64, u32, u64, vp]),
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
@@ -360,6 +361,18 @@ class Arena:
                 self._p = None
         except Exception:
             pass
+
+
+def arena_place(arena: "Arena", span: int, step: int, stream=None):
+    """kmws_arena_place: byte offset inside `arena` (multiples of `step`) where an
+    in-place split-8 unmask of `span` bytes runs fastest, and the probed rates
+    {offset: fraction of 8 TB/s}.  The arena's bytes are unchanged."""
+    k = (arena.nbytes - span) // step + 1 if span <= arena.nbytes else 0
+    fr = (C.c_float * max(k, 1))()
+    r = lib().kmws_arena_place(arena._p, arena.nbytes, span, step, _stream_handle(stream), fr, k)
+    if r < 0:
+        raise RuntimeError(f"kmws_arena_place failed with kmws_status {r}")
+    return int(r), {i * step: round(float(fr[i]), 4) for i in range(k)}
 
 
 def unmask_workspace_size(span: int) -> int:

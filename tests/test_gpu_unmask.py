@@ -254,3 +254,47 @@ def test_arena_alloc_unmask_roundtrip(torch_dev):
     assert ws.status() == 0 and kmws.check_unmasked(a.tensor, 77, descs) == 0
     del a
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("span_mib,step_mib,arena_mib", [(64, 32, 160), (1, 1, 3), (96, 48, 96)])
+def test_arena_place_picks_an_offset_and_leaves_bytes(torch_dev, span_mib, step_mib, arena_mib):
+    """kmws_arena_place: returns one of the probed offsets (multiples of step,
+    offset + span inside the arena), one rate per offset, and the arena's bytes
+    unchanged (the probe XORs every region twice); the batch placed there
+    unmasks bit-exactly.  A span that is not a whole number of 64 KiB probe
+    frames is covered too (96 MiB / 48 MiB steps: 1 offset)."""
+    torch = torch_dev
+    from kuma_amd import kmws
+    span, step = span_mib << 20, step_mib << 20
+    a = kmws.Arena(arena_mib << 20)
+    kmws.fill_synthetic(a.tensor, 4242)
+    torch.cuda.synchronize()
+    off, probe = kmws.arena_place(a, span, step)
+    assert sorted(probe) == list(range(0, (arena_mib << 20) - span + 1, step))
+    assert off in probe and off % step == 0 and off + span <= a.nbytes
+    assert all(v > 0 for v in probe.values())
+    n = a.nbytes // 65536  # nothing changed anywhere in the arena
+    d_all = torch.zeros((n, 2), dtype=torch.int64, device="cuda")
+    assert kmws.check_unmasked(a.tensor, 4242, d_all) == 0
+    L = 65536 - 7
+    descs = torch.empty((span // 65536, 2), dtype=torch.int64, device="cuda")
+    kmws.fill_uniform_descs(descs, 65536, L, 17)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span))
+    view = a.tensor[off:off + span]
+    kmws.unmask_batch(view, descs, ws, span)
+    torch.cuda.synchronize()
+    assert ws.status() == 0 and kmws.check_unmasked(view, 4242 + (off >> 3), descs) == 0
+
+
+@pytest.mark.gpu
+def test_arena_place_rejects_bad_arguments(torch_dev):
+    import ctypes as C
+    from kuma_amd import kmws
+    a = kmws.Arena(4 << 20)
+    lib = kmws.lib()
+    assert lib.kmws_arena_place(a._p, a.nbytes, 8 << 20, 1 << 20, None, None, 0) == kmws.ERR_INVALID_PARAM  # span > arena
+    assert lib.kmws_arena_place(a._p, a.nbytes, 1 << 20, 0, None, None, 0) == kmws.ERR_INVALID_PARAM        # step 0
+    assert lib.kmws_arena_place(a._p, a.nbytes, 1 << 20, 24, None, None, 0) == kmws.ERR_INVALID_PARAM       # step % 16
+    assert lib.kmws_arena_place(None, a.nbytes, 1 << 20, 1 << 20, None, None, 0) == kmws.ERR_INVALID_PARAM
+    assert lib.kmws_arena_place(a._p, a.nbytes, 0, 1 << 20, None, None, 0) == kmws.ERR_INVALID_PARAM
