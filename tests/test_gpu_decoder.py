@@ -249,3 +249,26 @@ def test_deferred_ring_zero_copy():
     for c in range(nconn):
         assert rets[c] == want[c][0]
         assert got[c] == want[c][1]
+
+
+@pytest.mark.parametrize("length,chunk", [(10485760, 65536), (10485760, 0), (10485761, 65536), (10485759, 1 << 20)])
+def test_max_frame_length_through_gpu_decoder(length, chunk):
+    """The decoder's cap WS_MAX_FRAME_DATA_LENGTH = 10 MiB (WSHandler.cpp:110,
+    :192-196): a masked 10 MiB frame (127-class header) is unmasked on the GPU
+    and delivered as the reference delivers it, whole or fed in 64 KiB / 1 MiB
+    reads (reassembled across reads); 10 MiB + 1 is INVALID_LENGTH (6) on both."""
+    rng = random.Random(length ^ chunk)
+    key = bytes(rng.randrange(256) for _ in range(4))
+    payload = bytes(rng.randrange(256) for _ in range(997)) * (length // 997) + bytes(length % 997)
+    hdr = orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=1, maskey=key, length=length))
+    stream = hdr + orc.mask_bytes(key, payload) + orc.encode_header(orc.Hdr(fin=1, opcode=9, mask=1, maskey=key,
+                                                                             length=3)) + orc.mask_bytes(key, b"end")
+    want = run_oracle(stream, kmws.SERVER, chunk, inplace=True)
+    got = run_kmws(stream, kmws.SERVER, chunk, inplace=True)
+    assert got[0] == want[0]
+    assert got[1] == want[1]
+    assert got[2] == want[2]
+    if length <= 10485760:
+        assert want[0][-1] == 0 and len(want[1]) == 2 and want[1][0][-1] == payload
+    else:
+        assert 6 in want[0] and want[1] == []

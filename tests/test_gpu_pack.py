@@ -35,6 +35,8 @@ def frames(rng, kind, n):
         lens = rng.integers(0, 9, size=n)
     elif kind == "frag4k":  # cfg4: 16 x 4 KiB per message
         lens = np.full(n, 4096)
+    elif kind == "max":  # the decoder's cap WS_MAX_FRAME_DATA_LENGTH (WSHandler.cpp:110) and neighbours
+        lens = np.resize(np.array([10485760, 3, 10485759, 0, 10485760 - 13, 10485760]), n)
     else:
         raise ValueError(kind)
     fin = rng.integers(0, 2, size=n)
@@ -85,11 +87,11 @@ def gpu_encode(T, src, offs, lens, flags, keys, cap=None):
     return dst.cpu().numpy(), wire_off.cpu().numpy(), ws.status(), total
 
 
-@pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k"])
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k", "max"])
 @pytest.mark.parametrize("aligned", [True, False])
 def test_encode_parity(T, kind, aligned):
     rng = np.random.default_rng(abs(hash((kind, aligned))) % 2**32)
-    n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320}[kind]
+    n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6}[kind]
     lens, flags, keys = frames(rng, kind, n)
     src, offs = src_arena(rng, lens, aligned)
     want, want_off = orc.encode_batch(src, offs, lens, flags, keys)
@@ -122,11 +124,11 @@ def wire_and_offsets(rng, kind, n, mode_mask=1):
     return wire, wire_off, src, offs, lens, flags, keys
 
 
-@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny"])
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max"])
 def test_unpack_gather_roundtrip(T, kind):
     from kuma_amd import kmws
     rng = np.random.default_rng(abs(hash(kind)) % 2**32)
-    wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, kind, 250)
+    wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, kind, 250 if kind != "max" else 6)
     hdr, used = kmws.find_headers(bytes(wire))
     # CLOSE frames stop the reference parser: cut the batch there like it does
     assert hdr == [int(x) for x in wire_off[:len(hdr)]]
