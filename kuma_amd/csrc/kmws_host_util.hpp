@@ -92,6 +92,7 @@ public:
             (void)hipHostFree(h_);
         }
         h_ = p;
+        dv_h_ = static_cast<uint8_t*>(device_view(h_));
         cap_ = c;
         return KMWS_OK;
     }
@@ -154,7 +155,7 @@ public:
                 h_piece_[k++] = PieceRec{(uint32_t)i, (uint32_t)j};
         }
         if (p1) {
-            uint8_t* dv = static_cast<uint8_t*>(device_view(h_));
+            uint8_t* dv = dv_h_;  // device view of the staging area, taken when it was allocated
             if (!dv) return KMWS_ERR_FAILED;
             st = launch_unmask_pieces(dv, dv_desc_, dv_piece_, (uint32_t)p1, stream_);
             if (st != KMWS_OK) return st;
@@ -213,6 +214,7 @@ private:
     int dev_ok_ = -1;
     hipStream_t stream_ = nullptr;
     uint8_t* h_ = nullptr;
+    uint8_t* dv_h_ = nullptr;
     size_t cap_ = 0, len_ = 0;
     std::vector<kmws_desc> descs_;
     kmws_desc* h_desc_ = nullptr;   // pinned, read by the kernel over PCIe

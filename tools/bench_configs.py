@@ -52,18 +52,24 @@ def cfg1(reps: int):
     wire = bytes(wire)
     chunk = 64 * 1024
 
+    # Every decoder / batch is long-lived, as on an event loop (one per
+    # connection / loop thread): created once, warmed by one untimed pass (its
+    # pinned staging grows to size), then the best of `reps` timed passes.
     def run(create, feed, destroy):
+        d = create()
+        bufs = [bytearray(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
+        cbufs = [(C.c_uint8 * len(b)).from_buffer(b) for b in bufs]
         best = 1e9
-        for _ in range(reps):
-            d = create()
-            bufs = [bytearray(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
-            cbufs = [(C.c_uint8 * len(b)).from_buffer(b) for b in bufs]
+        for rep in range(reps + 1):
+            for i, b in enumerate(bufs):  # fresh masked bytes (the decoder unmasks in place)
+                b[:] = wire[i * chunk:i * chunk + len(b)]
             t0 = time.perf_counter()
             for b, cb in zip(bufs, cbufs):
                 r = feed(d, cb, len(b))
                 assert r in (0, 1), r
-            best = min(best, time.perf_counter() - t0)
-            destroy(d)
+            if rep:
+                best = min(best, time.perf_counter() - t0)
+        destroy(d)
         return best
 
     O = orc.lib()
@@ -81,24 +87,26 @@ def cfg1(reps: int):
         res["product_decoder_sync"] = {"GiB_s": n * L / t_gpu / 2**30, "us_per_frame": t_gpu / n * 1e6,
                                        "best_of": reps,
                                        "note": "kmws_decoder_feed: host parse + one GPU unmask per 64 KiB read "
-                                               "(pageable chunk -> pinned staging, zero-copy kernel)"}
+                                               "(pageable chunk -> pinned staging, zero-copy kernel); bounded "
+                                               "below by one HIP launch + stream sync per read"}
         # deferred: every read of the burst fed, ONE flush (one GPU batch per loop iteration)
         nullcb = C.cast(None, kmws.FRAME_CB)
+        bufs = [bytes(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
+        cbufs = [(C.c_uint8 * len(x)).from_buffer_copy(x) for x in bufs]
+        d = K.kmws_decoder_create(1, 0)
+        b = K.kmws_rx_batch_create(0)
         best = 1e9
-        for _ in range(reps):
-            d = K.kmws_decoder_create(1, 0)
-            b = K.kmws_rx_batch_create(0)
-            bufs = [bytes(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
-            cbufs = [(C.c_uint8 * len(x)).from_buffer_copy(x) for x in bufs]
+        for rep in range(reps + 1):
             t0 = time.perf_counter()
             for x, cb in zip(bufs, cbufs):
                 r = K.kmws_decoder_feed_deferred(d, b, cb, len(x), nullcb, None)
                 assert r in (0, 1), r
             got = K.kmws_rx_batch_flush(b)
-            best = min(best, time.perf_counter() - t0)
+            if rep:
+                best = min(best, time.perf_counter() - t0)
             assert got == n, got
-            K.kmws_rx_batch_destroy(b)
-            K.kmws_decoder_destroy(d)
+        K.kmws_rx_batch_destroy(b)
+        K.kmws_decoder_destroy(d)
         res["product_decoder_deferred"] = {"GiB_s": n * L / best / 2**30, "us_per_frame": best / n * 1e6,
                                            "best_of": reps,
                                            "note": "kmws_decoder_feed_deferred per read + one kmws_rx_batch_flush"}
@@ -107,11 +115,11 @@ def cfg1(reps: int):
         import torch
         ring = torch.empty(len(wire) + 64 * 128, dtype=torch.uint8).pin_memory()
         wire_t = torch.frombuffer(bytearray(wire), dtype=torch.uint8)
+        d = K.kmws_decoder_create(1, 0)
+        b = K.kmws_rx_batch_create(0)
+        assert K.kmws_rx_batch_attach_ring(b, ring.data_ptr(), ring.numel()) == 0
         best = 1e9
-        for _ in range(reps):
-            d = K.kmws_decoder_create(1, 0)
-            b = K.kmws_rx_batch_create(0)
-            assert K.kmws_rx_batch_attach_ring(b, ring.data_ptr(), ring.numel()) == 0
+        for rep in range(reps + 1):
             offs = []
             w = 0
             for i in range(0, len(wire), chunk):
@@ -125,10 +133,11 @@ def cfg1(reps: int):
                 r = K.kmws_decoder_feed_deferred(d, b, base + o, m, nullcb, None)
                 assert r in (0, 1), r
             got = K.kmws_rx_batch_flush(b)
-            best = min(best, time.perf_counter() - t0)
+            if rep:
+                best = min(best, time.perf_counter() - t0)
             assert got == n, got
-            K.kmws_rx_batch_destroy(b)
-            K.kmws_decoder_destroy(d)
+        K.kmws_rx_batch_destroy(b)
+        K.kmws_decoder_destroy(d)
         res["product_decoder_deferred_ring"] = {"GiB_s": n * L / best / 2**30, "us_per_frame": best / n * 1e6,
                                                 "best_of": reps,
                                                 "note": "reads in a pinned ring attached to the batch; one flush"}
