@@ -1,0 +1,171 @@
+// Latency probe (dev tool): host -> GPU -> host round trips for small zero-copy
+// jobs, (a) one kernel launch + hipStreamSynchronize per job, (b) a resident
+// "service" grid polling a mailbox in coherent pinned host memory.  Each job
+// XORs `bytes` of a pinned host buffer in place (like one 64 KiB socket read).
+// Safety: the service grid exits on a quit flag, after 20 ms without a job, or
+// after 5 s in total, whichever comes first; the host waits at most 1 s per job.
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/doorbell_probe tools/doorbell_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Mailbox {
+    uint64_t seq;        // host -> GPU
+    uint64_t pad0[15];
+    uint64_t done;       // GPU -> host
+    uint64_t pad1[15];
+    uint32_t quit;
+    uint32_t words;      // job size in 16-byte words
+    uint64_t pad2[15];
+};
+
+__global__ void xor_once(u32x4* buf, uint32_t words)
+{
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < words; w += gridDim.x * blockDim.x)
+        buf[w] ^= u32x4{0x01020304u, 0x05060708u, 0x090a0b0cu, 0x0d0e0f10u};
+}
+
+__device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
+
+#ifndef RELAXED
+#define RELAXED 0
+#endif
+__global__ void service(Mailbox* mb, u32x4* buf, unsigned int* counter, uint64_t idle_ticks, uint64_t life_ticks)
+{
+    __shared__ uint64_t s_seq;
+    __shared__ uint32_t s_quit, s_words;
+    const uint64_t t_start = now_ticks();
+    uint64_t last = 0, t_last = t_start;
+    uint32_t jobs = 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            s_seq = __hip_atomic_load(&mb->seq, RELAXED ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_quit = __hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_words = __hip_atomic_load(&mb->words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const uint64_t seq = s_seq;
+        const uint32_t quit = s_quit, words = s_words;
+        __syncthreads();
+        if (quit) break;
+        const uint64_t t = now_ticks();
+        if (seq != last) {
+            for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < words; w += gridDim.x * blockDim.x) {
+                u32x4 v = __builtin_nontemporal_load(buf + w);
+                __builtin_nontemporal_store(v ^ u32x4{0x01020304u, 0x05060708u, 0x090a0b0cu, 0x0d0e0f10u}, buf + w);
+            }
+            __syncthreads();
+            ++jobs;
+            if (threadIdx.x == 0) {
+#if RELAXED
+                // coherent (uncached) host memory: wait for this block's stores, count at agent scope
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                const unsigned int old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (old + 1 == jobs * gridDim.x)
+                    __hip_atomic_store(&mb->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+                __atomic_thread_fence(__ATOMIC_RELEASE);  // this block's stores before its count
+                const unsigned int old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (old + 1 == jobs * gridDim.x)
+                    __hip_atomic_store(&mb->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+            }
+            last = seq;
+            t_last = t;
+        } else {
+            if (t - t_last > idle_ticks || t - t_start > life_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+
+static double us_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static double median(std::vector<double> v)
+{
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+#include <algorithm>
+
+int main(int argc, char** argv)
+{
+    const uint32_t bytes = argc > 1 ? atoi(argv[1]) : 65536;
+    const int grid = argc > 2 ? atoi(argv[2]) : 8;
+    const uint32_t words = bytes / 16;
+    hipStream_t s, ss;
+    (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&ss, hipStreamNonBlocking);
+    u32x4 *hbuf = nullptr, *dbuf = nullptr;
+    Mailbox *mb = nullptr, *dmb = nullptr;
+    unsigned int* counter = nullptr;
+    if (hipHostMalloc((void**)&hbuf, bytes, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void**)&mb, sizeof(Mailbox), hipHostMallocCoherent) != hipSuccess ||
+        hipMalloc((void**)&counter, 4) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    (void)hipHostGetDevicePointer((void**)&dbuf, hbuf, 0);
+    (void)hipHostGetDevicePointer((void**)&dmb, mb, 0);
+    memset(hbuf, 0x5a, bytes);
+    memset(mb, 0, sizeof(Mailbox));
+    (void)hipMemset(counter, 0, 4);
+    (void)hipDeviceSynchronize();
+
+    // (a) launch + sync per job
+    std::vector<double> ta;
+    for (int i = 0; i < 400; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(xor_once, dim3(grid), dim3(256), 0, s, dbuf, words);
+        (void)hipStreamSynchronize(s);
+        ta.push_back(us_since(t0));
+    }
+    // (b) resident service grid
+    mb->words = words;
+    hipLaunchKernelGGL(service, dim3(grid), dim3(256), 0, ss, dmb, dbuf, counter, 2000000ull /*20 ms*/,
+                       500000000ull /*5 s*/);
+    std::vector<double> tb;
+    int lost = 0;
+    for (int i = 0; i < 400; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        const uint64_t seq = (uint64_t)i + 1;
+        std::atomic_thread_fence(std::memory_order_release);
+        __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+        bool ok = false;
+        while (us_since(t0) < 1e6) {
+            if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) {
+                ok = true;
+                break;
+            }
+        }
+        if (!ok) {
+            ++lost;
+            break;
+        }
+        tb.push_back(us_since(t0));
+    }
+    __atomic_store_n(&mb->quit, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(ss);
+    // 800 XOR passes with the same pattern (even): the buffer is back to 0x5a
+    bool intact = true;
+    const uint8_t* hb = reinterpret_cast<const uint8_t*>(hbuf);
+    for (uint32_t i = 0; i < bytes; ++i) intact &= hb[i] == 0x5a;
+    printf("{\"bytes\": %u, \"grid\": %d, \"launch_sync_us\": %.2f, \"service_rtt_us\": %.2f, \"service_jobs\": %zu, "
+           "\"lost\": %d, \"bytes_intact\": %s}\n",
+           bytes, grid, median(ta), tb.empty() ? -1.0 : median(tb), tb.size(), lost, intact ? "true" : "false");
+    (void)hipHostFree(hbuf);
+    (void)hipHostFree(mb);
+    (void)hipFree(counter);
+    return lost ? 2 : 0;
+}
