@@ -244,6 +244,136 @@ def cfg3(reps: int, gib: float):
             "note": "decode is descriptor-indexed: header offsets = the receiver's host parse (here wire_off)"}
 
 
+def pinned_host(torch, nbytes: int):
+    """Exactly nbytes of page-locked host memory: numpy pages (touched, so they
+    are resident) registered with hipHostRegister.  torch's pin_memory() would
+    round the request up to a power of two in its caching host allocator (two
+    8 GiB buffers become 32 GiB pinned), and the copy engines ran at a third of
+    the PCIe rate over such large pinned sets."""
+    a = np.empty(nbytes, dtype=np.uint8)
+    a.fill(0)
+    rt = torch.cuda.cudart()
+    if int(rt.cudaHostRegister(a.ctypes.data, nbytes, 0)) != 0:
+        raise RuntimeError("hipHostRegister failed")
+    t = torch.from_numpy(a)
+    assert t.is_pinned()
+    return t, a
+
+
+def cfg3_e2e(gib: float, chunk_mib: int, reps: int):
+    """BASELINE configs[2] end to end (SURVEY 8 d row 3 ii): a pinned host
+    buffer of plain Zipf payloads (dense, back to back) -> per chunk of frames
+    (<= chunk_mib of payload): H2D -> kmws_encode_batch (header pack + mask) ->
+    kmws_unpack_headers -> kmws_gather_unmask -> D2H into a second pinned host
+    buffer, which must equal the input.  Three slots on three streams (H2D ||
+    device work || D2H, ordered by events), as kmws_pipeline's ring."""
+    import torch
+    from kuma_amd import kmws
+    rng = np.random.default_rng(SEED ^ 0xE2E)
+    lens = zipf_lens(rng, 4_000_000)
+    n = int(np.searchsorted(np.cumsum(lens), gib * 2**30)) + 1
+    lens = lens[:n]
+    P = int(lens.sum())
+    pay_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)  # dense host layout
+    flags = (0x80 | np.where(np.arange(n) % 2 == 0, 1, 2) | 0x100).astype(np.int16)
+    keys = splitmix_keys(SEED ^ 5, n).astype(np.int64)
+    hl = np.where(lens <= 125, 2, np.where(lens <= 65535, 4, 10)) + 4
+    # chunks of whole frames, <= chunk bytes of payload each; source offsets relative
+    # to the chunk's 16-B aligned host start
+    cb = chunk_mib << 20
+    cuts = [0]
+    while cuts[-1] < n:
+        a = cuts[-1]
+        cuts.append(max(a + 1, int(np.searchsorted(pay_off, pay_off[a] + cb, side="right")) - 1))
+    cuts[-1] = n
+    chunks = []
+    rel = np.empty(n, dtype=np.int64)
+    for a, b in zip(cuts, cuts[1:]):
+        h0 = int(pay_off[a]) & ~15
+        rel[a:b] = pay_off[a:b] - h0
+        chunks.append((a, b, h0, int(pay_off[b]) - h0, int(pay_off[b] - pay_off[a]), int((hl[a:b] + lens[a:b]).sum())))
+    dev = torch.device("cuda")
+    host_src, _keep_src = pinned_host(torch, P + 32)
+    host_dst, _keep_dst = pinned_host(torch, P + 32)
+    tmp = torch.empty(P + 32, dtype=torch.uint8, device=dev)
+    kmws.fill_synthetic(tmp, SEED ^ 9)
+    host_src.copy_(tmp)
+    del tmp
+    host_dst.zero_()
+    descs = kmws.make_descs(rel, lens, keys)
+    fl = torch.from_numpy(flags).to(dev)
+    nmax = max(b - a for a, b, *_ in chunks)
+    spanmax = max(c[3] for c in chunks)
+    wmax = max(c[5] for c in chunks)
+    S = 3
+    slots = []
+    for _ in range(S):
+        slots.append({
+            "src": torch.empty(spanmax + 32, dtype=torch.uint8, device=dev),
+            "wire": torch.empty(wmax + 32, dtype=torch.uint8, device=dev),
+            "dst": torch.empty(cb + 32, dtype=torch.uint8, device=dev),
+            "wire_off": torch.empty(nmax + 1, dtype=torch.int64, device=dev),
+            "out_desc": torch.empty((nmax, 2), dtype=torch.int64, device=dev),
+            "dst_off": torch.empty(nmax + 1, dtype=torch.int64, device=dev),
+            "ws_e": kmws.Workspace(kmws.copy_workspace_size(nmax, wmax + 32)),
+            "ws_u": kmws.Workspace(16),
+            "ws_g": kmws.Workspace(kmws.copy_workspace_size(nmax, cb + 32)),
+            "h2d": torch.cuda.Event(), "comp": torch.cuda.Event(), "d2h": torch.cuda.Event(),
+        })
+    s_h2d, s_comp, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(chunks) + 1)]
+    issue = [0.0]
+    torch.cuda.synchronize()
+
+    def one_pass():
+        marks[0].record(s_d2h)
+        for c, (a, b, h0, span, pc, wc) in enumerate(chunks):
+            sl = slots[c % S]
+            nc = b - a
+            if c >= S:
+                # the slot's previous chunk has left the device: a host wait keeps at most S
+                # chunks of work queued (a deep queue of cross-stream waits stalled the copies)
+                sl["d2h"].synchronize()
+            with torch.cuda.stream(s_h2d):
+                sl["src"][:span].copy_(host_src[h0:h0 + span], non_blocking=True)
+                sl["h2d"].record(s_h2d)
+            s_comp.wait_event(sl["h2d"])
+            kmws.encode_batch(sl["src"], descs[a:b], fl[a:b], sl["wire"], sl["wire_off"][:nc + 1], sl["ws_e"],
+                              stream=s_comp)
+            kmws.unpack_headers(sl["wire"], sl["wire_off"][:nc], kmws.SERVER, sl["out_desc"][:nc], None, None,
+                                sl["ws_u"], wire_len=wc, stream=s_comp)
+            kmws.gather_unmask(sl["wire"], sl["out_desc"][:nc], sl["dst"], sl["dst_off"][:nc + 1], sl["ws_g"],
+                               stream=s_comp)
+            sl["comp"].record(s_comp)
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(sl["comp"])
+                host_dst[int(pay_off[a]):int(pay_off[b])].copy_(sl["dst"][:pc], non_blocking=True)
+                sl["d2h"].record(s_d2h)
+                marks[c + 1].record(s_d2h)
+        issue[0] = time.perf_counter()
+        torch.cuda.synchronize()
+
+    one_pass()  # warm
+    ok = bool(torch.equal(host_dst[:P], host_src[:P]))
+    st = [sl[w].status() for sl in slots for w in ("ws_e", "ws_u", "ws_g")]
+    best, issue_s = 1e9, 0.0
+    for _ in range(reps):
+        host_dst[:P].zero_()
+        t0 = time.perf_counter()
+        one_pass()
+        t1 = time.perf_counter()
+        if t1 - t0 < best:
+            best, issue_s = t1 - t0, issue[0] - t0
+    ok = ok and bool(torch.equal(host_dst[:P], host_src[:P])) and not any(st)
+    gaps = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(len(chunks)))  # last pass, ms per chunk
+    qs = {q: round(gaps[int(q * (len(gaps) - 1))], 3) for q in (0.1, 0.5, 0.9)}
+    return {"config": "cfg3_e2e", "frames": n, "payload_bytes": P, "chunks": len(chunks), "chunk_MiB": chunk_mib,
+            "slots": S, "payload_GiB_s": P / best / 2**30, "pcie_bytes": 2 * P, "verified": ok,
+            "chunk_ms_quantiles": qs, "host_issue_s": round(issue_s, 4), "total_s": round(best, 4),
+            "note": "pinned host plain payload -> H2D -> encode (pack+mask) -> unpack -> gather-unmask -> D2H, "
+                    "3 slots on 3 streams; PCIe-bound (each payload byte crosses twice)"}
+
+
 # ------------------------------------------------------------------ cfg4
 def cfg4(reps: int, messages: int):
     import torch
@@ -339,7 +469,7 @@ def e2e(gib: float, chunk_mib: int, depth: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg3", "cfg4", "e2e"])
+    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cfg3-gib", type=float, default=8.0)
     ap.add_argument("--cfg4-messages", type=int, default=262144)
@@ -352,6 +482,8 @@ def main():
             r = cfg1(max(a.reps, 10))
         elif w == "cfg3":
             r = cfg3(a.reps, a.cfg3_gib)
+        elif w == "cfg3_e2e":
+            r = cfg3_e2e(a.cfg3_gib, a.e2e_chunk_mib, min(a.reps, 3))
         elif w == "cfg4":
             r = cfg4(a.reps, a.cfg4_messages)
         else:
