@@ -7,6 +7,9 @@ produces the measured numbers), verified on the device:
         (index-gather check independent of the kernels);
   cfg4  16 x 4 KiB fragment chains (a-12): pack -> unpack (flags == the
         packed ones, no WSError) -> in-place unmask == the source payloads;
+  cfg3_e2e  pinned host Zipf payloads -> H2D -> encode -> unpack ->
+        gather-unmask -> D2H == the input, every byte (chunks of whole frames
+        on three slots, frames straddling no chunk);
   e2e   pinned host wire image unmasked an even number of times (zero-copy
         and SDMA ring) == its initial bytes, every byte.
 
@@ -45,3 +48,8 @@ def test_cfg4_roundtrip(bc):
 def test_e2e_pipeline_roundtrip(bc):
     r = bc.e2e(0.25, 16, 3)
     assert r["verified"]
+
+
+def test_cfg3_e2e_roundtrip(bc):
+    r = bc.cfg3_e2e(0.25, 8, 1)  # 8 MiB chunks: ~32 chunks, every slot reused many times
+    assert r["verified"] and r["chunks"] > 6
