@@ -7,9 +7,10 @@
 //   1. scan_reduce / scan_partials / scan_emit: one exclusive scan of two
 //      per-frame values -- the wire size (2/4/10 + 4*mask + len) -> wire_off,
 //      and an upper bound on the frame's wave units -> unit slot bases;
-//   2. unit_rec: one 32-byte record per wave unit (slots written coalesced);
-//      edge_kernel: the few words around each frame boundary (header bytes,
-//      the next frame's first bytes), composed byte-exactly;
+//   2. rec_edge_kernel, one grid for two independent jobs: one 32-byte record
+//      per wave unit (slots written coalesced), and the few words around each
+//      frame boundary (header bytes, the next frame's first bytes), composed
+//      byte-exactly;
 //   3. copy_kernel: one wave per unit of a frame's owned 64-byte granules;
 //      interior words are loaded, funnel-shifted and XORed with the rotated
 //      key, edge words are merged in; every granule is written once, by one
@@ -303,7 +304,7 @@ __device__ __forceinline__ u32x4 byte_range(int lo, int hi)
 //     from its neighbour;
 //   edge words -- at most one holding the header's end, and the words after the
 //     payload's end up to the granule's end (the next frames' first bytes) --
-//     are composed byte-exactly beforehand by edge_kernel, one thread per word,
+//     are composed byte-exactly beforehand (edge_block), one thread per word,
 //     into a per-frame buffer; the wave loads them (one lane per word) and moves
 //     them into their store lanes with a lane permute.
 // Every output byte in [0, total) is written exactly once.
@@ -488,18 +489,15 @@ __device__ u32x4 compose_word(uint64_t a, uint32_t f, uint32_t n, const FrameGeo
 // Frame f owns slots [ubase[f], ubase[f+1]); slots past its exact unit count
 // are marked empty.  Also the capacity check (status set if total > cap).
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __restrict__ start,
-                                                          const uint64_t* __restrict__ ubase,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags, uint32_t n,
-                                                          uint64_t cap, UnitRec* __restrict__ rec,
-                                                          WsHead* __restrict__ head)
+__device__ __forceinline__ void unit_rec_block(uint32_t blk, uint32_t* s_ub, const uint64_t* __restrict__ start,
+                                               const uint64_t* __restrict__ ubase, const kmws_desc* __restrict__ d,
+                                               const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
+                                               UnitRec* __restrict__ rec, WsHead* __restrict__ head)
 {
-    __shared__ uint32_t s_ub[kBlock + 1];
-    const uint32_t f0 = blockIdx.x * kBlock;
+    const uint32_t f0 = blk * kBlock;
     const uint64_t total = start[n];
     if (total > cap) {  // records would not fit the workspace; the copy waves see the status
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&head->status, kStatusBadDesc);
+        if (blk == 0 && threadIdx.x == 0) atomicOr(&head->status, kStatusBadDesc);
         return;
     }
     const uint32_t nf = n - f0 < (uint32_t)kBlock ? n - f0 : (uint32_t)kBlock;
@@ -549,15 +547,13 @@ __global__ void __launch_bounds__(kBlock) unit_rec_kernel(const uint64_t* __rest
 // (frame, q) into edge[f * kEdgeWords + q].
 constexpr int kEdgeFramesPerBlock = kBlock / kEdgeWords;  // 51 frames, 255 threads
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) edge_kernel(const uint8_t* __restrict__ src,
-                                                      const uint64_t* __restrict__ start,
-                                                      const kmws_desc* __restrict__ d,
-                                                      const uint16_t* __restrict__ flags, uint32_t n,
-                                                      uint64_t cap, u32x4* __restrict__ edge,
-                                                      const WsHead* __restrict__ head, uint64_t block_base)
+__device__ __forceinline__ void edge_block(uint64_t blk, const uint8_t* __restrict__ src,
+                                           const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
+                                           const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
+                                           u32x4* __restrict__ edge, const WsHead* __restrict__ head)
 {
     const uint32_t t = threadIdx.x;
-    const uint64_t f64 = (block_base + blockIdx.x) * kEdgeFramesPerBlock + t / kEdgeWords;
+    const uint64_t f64 = blk * kEdgeFramesPerBlock + t / kEdgeWords;
     if (t >= (uint32_t)(kEdgeFramesPerBlock * kEdgeWords) || f64 >= n) return;
     const uint32_t f = (uint32_t)f64, q = t % kEdgeWords;
     // total, status and the three frames' geometry: one latency level
@@ -574,6 +570,28 @@ __global__ void __launch_bounds__(kBlock) edge_kernel(const uint8_t* __restrict_
     else if (q < head_f + tail) word = w.ihi + (q - head_f);
     else return;
     edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, g, fl, src, start, d, flags);
+}
+
+// Unit records and edge words in one grid (they are independent, and the
+// record blocks alone are too few to fill the chip): virtual block v < rec_blocks
+// writes records, v >= rec_blocks composes edge words (edge block v - rec_blocks);
+// v = vbase + blockIdx.x, the grid being cut at 2^31 work-items per launch.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) rec_edge_kernel(const uint8_t* __restrict__ src,
+                                                          const uint64_t* __restrict__ start,
+                                                          const uint64_t* __restrict__ ubase,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          uint64_t cap, UnitRec* __restrict__ rec,
+                                                          u32x4* __restrict__ edge, WsHead* __restrict__ head,
+                                                          uint64_t rec_blocks, uint64_t vbase)
+{
+    __shared__ uint32_t s_ub[kBlock + 1];
+    const uint64_t v = vbase + blockIdx.x;
+    if (v < rec_blocks)
+        unit_rec_block<HEADERS>((uint32_t)v, s_ub, start, ubase, d, flags, n, cap, rec, head);
+    else
+        edge_block<HEADERS>(v - rec_blocks, src, start, d, flags, n, cap, edge, head);
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
@@ -623,7 +641,7 @@ struct UnitRegs {
 // addresses clamped to [ilo, ihi - 1] (a unit without interior words reads
 // src's first word instead); the next source word comes from the neighbour
 // lane, lane 63 takes it from lane 0 of the next instruction, and the last
-// interior word from `ex`.  Edge words (composed by edge_kernel: [klo, ilo)
+// interior word from `ex`.  Edge words (composed by edge_block: [klo, ilo)
 // then [ihi, khi)): one per lane, index clamped.
 __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const uint8_t* __restrict__ src,
                                            const u32x4* __restrict__ edge, UnitRegs& R)
@@ -901,13 +919,12 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
                                const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t fb = (n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(unit_rec_kernel<HEADERS>, dim3(fb), dim3(kBlock), 0, s, start, c.ubase, d, flags, n, cap,
-                       c.rec, c.head);
     const uint64_t eb = ((uint64_t)n + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
-    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;  // stay below 2^32 work-items per launch
-    for (uint64_t b0 = 0; b0 < eb; b0 += kMaxBlocks)
-        hipLaunchKernelGGL(edge_kernel<HEADERS>, dim3((uint32_t)(eb - b0 < kMaxBlocks ? eb - b0 : kMaxBlocks)),
-                           dim3(kBlock), 0, s, src, start, d, flags, n, cap, c.edge, c.head, b0);
+    constexpr uint64_t kMaxBlocks = (1ull << 31) / kBlock;  // stay below 2^31 work-items per launch
+    for (uint64_t v0 = 0, nv = fb + eb; v0 < nv; v0 += kMaxBlocks)
+        hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
+                           dim3(kBlock), 0, s, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
+                           (uint64_t)fb, v0);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
     // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
     // batches of small frames need every wave slot to hide their per-unit
