@@ -33,6 +33,7 @@ typedef int kmws_status;
 #define KMWS_ERR_INVALID_STATE    (-7)   /* KMError::INVALID_STATE */
 #define KMWS_ERR_INVALID_PARAM    (-8)   /* KMError::INVALID_PARAM */
 #define KMWS_ERR_BUFFER_TOO_SMALL (-17)  /* KMError::BUFFER_TOO_SMALL */
+#define KMWS_ERR_BUFFER_TOO_LONG  (-18)  /* KMError::BUFFER_TOO_LONG (a send of more than 128 segments) */
 #define KMWS_ERR_NOT_SUPPORTED    (-19)  /* KMError::NOT_SUPPORTED (no gfx950 device) */
 
 /* ---- codec results: WSError (src/ws/wsdefs.h:56-67) ---- */
@@ -149,6 +150,37 @@ int            kmws_rx_batch_pending(const kmws_rx_batch* b);
  * flush must stay unmodified until that flush.  NULL detaches. */
 kmws_status    kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes);
 void           kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec);
+
+/* ---- batched send path: one GPU batch per event-loop iteration (SURVEY f-2) ----
+ * WebSocket::Impl::sendWsFrame (WebSocketImpl.cpp:381-436) masks the caller's
+ * payload in place and packs the header, once per send.  A loop thread
+ * instead queues every send of the iteration with kmws_tx_batch_add -- the
+ * header is packed at once into hdr_out (length = (uint32_t) payload bytes,
+ * :390/:415, then encodeFrameHeader) and the payload segments are queued for
+ * masking with hdr->maskey when hdr->mask is set and the payload is not empty
+ * (kuma's client mode: mask = 1 and a fresh key per frame, :386/:411; keys are
+ * inputs here) -- and kmws_tx_batch_flush masks every queued payload in place
+ * with one GPU launch, key phase continuing across a frame's segments.  The
+ * segments must stay valid and unmodified until the flush; the iovec list for
+ * the socket is then [hdr_out, segments...] as in :419-431.  A send with more
+ * than 128 non-empty segments returns KMWS_ERR_BUFFER_TOO_LONG, and -- as in
+ * kuma, which masks before counting iovecs -- its payload is still masked at
+ * the flush.  Payloads over 4 GiB - 1 are refused (KMWS_ERR_INVALID_PARAM). */
+typedef struct kmws_tx_batch kmws_tx_batch;
+kmws_tx_batch* kmws_tx_batch_create(int device);      /* NULL without a gfx950 device */
+void           kmws_tx_batch_destroy(kmws_tx_batch* b);
+/* Returns the header length (2..14) or a negative kmws_status. */
+int            kmws_tx_batch_add(kmws_tx_batch* b, const kmws_frame_hdr* hdr, uint8_t* const* segs,
+                                 const size_t* lens, size_t nseg, uint8_t hdr_out[KMWS_MAX_HEADER_SIZE]);
+/* Masks every queued payload (one launch, synchronous); returns the number of
+ * frames masked, or a negative kmws_status.  The batch is empty afterwards. */
+int64_t        kmws_tx_batch_flush(kmws_tx_batch* b);
+int            kmws_tx_batch_pending(const kmws_tx_batch* b);
+/* Optional pinned send ring (hipHostMalloc / hipHostRegister) the loop builds
+ * its outgoing payloads in: segments inside it are masked in place there at
+ * flush (zero-copy, one launch), the others go through pinned staging.  Only
+ * while the batch is empty; NULL detaches. */
+kmws_status    kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ring_bytes);
 
 /* ======================= device batch entries ======================= */
 

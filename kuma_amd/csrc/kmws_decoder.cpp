@@ -14,6 +14,7 @@
 // fails the call with KMWS_ERR_NOT_SUPPORTED.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -425,6 +426,135 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
     }
     s->clear();
     return KMWS_OK;
+}
+
+// ---- batched send path (SURVEY f-2) ----
+
+struct kmws_tx_batch {
+    struct Seg {
+        uint8_t* p;
+        size_t len;
+    };
+    struct Frame {
+        size_t seg0, nseg;  // range in segs
+        size_t bytes;
+        uint32_t key;
+    };
+    PinnedStage stage;
+    std::vector<Seg> segs;
+    std::vector<Frame> frames;
+    size_t bytes = 0;
+    int device = 0;
+    uint8_t* ring = nullptr;  // caller's pinned send ring (optional)
+    size_t ring_bytes = 0;
+    std::vector<kmws_desc> ring_descs;
+    bool in_ring(const uint8_t* p, size_t n) const
+    {
+        return ring && p >= ring && n <= ring_bytes && (size_t)(p - ring) <= ring_bytes - n;
+    }
+};
+
+kmws_tx_batch* kmws_tx_batch_create(int device)
+{
+    kmws_tx_batch* b = new (std::nothrow) kmws_tx_batch();
+    if (!b) return nullptr;
+    b->device = device;
+    if (b->stage.init(device) != KMWS_OK) {
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+void kmws_tx_batch_destroy(kmws_tx_batch* b) { delete b; }
+
+int kmws_tx_batch_pending(const kmws_tx_batch* b) { return b ? (int)b->frames.size() : 0; }
+
+// sendWsFrame (WebSocketImpl.cpp:405-436) up to the socket write: length =
+// u32(chain length) (:415), header packed (:416), payload queued for masking
+// when the header says so and it is not empty (:410-414); more than 128
+// non-empty segments -> BUFFER_TOO_LONG after the mask, as kuma (:419-431).
+int kmws_tx_batch_add(kmws_tx_batch* b, const kmws_frame_hdr* hdr, uint8_t* const* segs, const size_t* lens,
+                      size_t nseg, uint8_t hdr_out[KMWS_MAX_HEADER_SIZE])
+{
+    if (!b || !hdr || !hdr_out || (nseg && (!segs || !lens))) return KMWS_ERR_INVALID_PARAM;
+    size_t plen = 0, nonempty = 0;
+    for (size_t i = 0; i < nseg; ++i) {
+        if (lens[i] && !segs[i]) return KMWS_ERR_INVALID_PARAM;
+        plen += lens[i];
+        nonempty += lens[i] != 0;
+    }
+    if (plen > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    kmws_frame_hdr h = *hdr;
+    h.length = (uint32_t)plen;
+    const int hl = kmws_encode_header(&h, hdr_out);
+    if (h.mask && plen > 0) {
+        uint32_t key;
+        std::memcpy(&key, h.maskey, 4);
+        b->frames.push_back(kmws_tx_batch::Frame{b->segs.size(), 0, plen, key});
+        for (size_t i = 0; i < nseg; ++i)
+            if (lens[i]) b->segs.push_back(kmws_tx_batch::Seg{segs[i], lens[i]});
+        b->frames.back().nseg = b->segs.size() - b->frames.back().seg0;
+        b->bytes += plen;
+    }
+    return 1 + nonempty > 129 ? KMWS_ERR_BUFFER_TOO_LONG : hl;
+}
+
+// kmws_tx_batch_attach_ring: segments inside it are masked there (zero-copy).
+kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ring_bytes)
+{
+    if (!b || (ring && !ring_bytes)) return KMWS_ERR_INVALID_PARAM;
+    if (!b->frames.empty()) return KMWS_ERR_INVALID_STATE;  // queued segments were classified already
+    if (ring && !device_view(ring)) return KMWS_ERR_INVALID_PARAM;  // must be pinned
+    b->ring = ring;
+    b->ring_bytes = ring ? ring_bytes : 0;
+    return KMWS_OK;
+}
+
+// One descriptor per segment, its key rotated by the frame bytes before it
+// (the phase continues across segments, WSHandler.cpp:312-322): segments in
+// the attached pinned ring are masked in place there, the others gathered
+// into pinned staging and scattered back; one launch per buffer.
+int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
+{
+    if (!b) return KMWS_ERR_INVALID_PARAM;
+    const int64_t nf = (int64_t)b->frames.size();
+    if (nf == 0) return 0;
+    PinnedStage& s = b->stage;
+    s.clear();
+    b->ring_descs.clear();
+    size_t staged = 0;
+    for (const kmws_tx_batch::Seg& g : b->segs)
+        if (!b->in_ring(g.p, g.len)) staged += g.len + 16;
+    kmws_status st = s.reserve(staged);
+    std::vector<size_t> offs(b->segs.size(), SIZE_MAX);
+    if (st == KMWS_OK) {
+        for (const kmws_tx_batch::Frame& fr : b->frames) {
+            size_t phase = 0;
+            for (size_t i = fr.seg0; i < fr.seg0 + fr.nseg; ++i) {
+                const kmws_tx_batch::Seg& g = b->segs[i];
+                const uint32_t key = __builtin_rotateright32(fr.key, 8u * (uint32_t)(phase & 3u));
+                if (b->in_ring(g.p, g.len)) {
+                    b->ring_descs.push_back(kmws_desc{(uint64_t)(g.p - b->ring), (uint32_t)g.len, key});
+                } else {
+                    uint8_t* dst = s.alloc(g.len, &offs[i]);
+                    std::memcpy(dst, g.p, g.len);
+                    s.add_desc(offs[i], (uint32_t)g.len, key);
+                }
+                phase += g.len;
+            }
+        }
+        st = b->ring_descs.empty() ? s.run() : s.run(b->ring, b->ring_bytes, &b->ring_descs);
+    }
+    if (st == KMWS_OK)
+        for (size_t i = 0; i < b->segs.size(); ++i)
+            if (offs[i] != SIZE_MAX) std::memcpy(b->segs[i].p, s.data() + offs[i], b->segs[i].len);
+    s.clear();
+    b->frames.clear();
+    b->segs.clear();
+    b->ring_descs.clear();
+    b->bytes = 0;
+    return st == KMWS_OK ? nf : (int64_t)st;
 }
 
 // ---- deferred delivery across calls and connections ----

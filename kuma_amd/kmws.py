@@ -18,7 +18,7 @@ from . import build as _build
 
 # ---- constants (include/kmws_gpu.h) ----
 OK, ERR_FAILED, ERR_INVALID_STATE, ERR_INVALID_PARAM = 0, -1, -7, -8
-ERR_BUFFER_TOO_SMALL, ERR_NOT_SUPPORTED = -17, -19
+ERR_BUFFER_TOO_SMALL, ERR_BUFFER_TOO_LONG, ERR_NOT_SUPPORTED = -17, -18, -19
 CLIENT, SERVER = 0, 1
 OP_CONTINUE, OP_TEXT, OP_BINARY, OP_CLOSE, OP_PING, OP_PONG = 0, 1, 2, 8, 9, 10
 WS_NOERR, WS_NEED_MORE_DATA, WS_INVALID_FRAME, WS_INVALID_LENGTH = 0, 1, 5, 6
@@ -38,6 +38,8 @@ EXPORTS = [
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
     "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place",
+    "kmws_tx_batch_create", "kmws_tx_batch_destroy", "kmws_tx_batch_add", "kmws_tx_batch_flush",
+    "kmws_tx_batch_pending", "kmws_tx_batch_attach_ring",
 ]
 
 
@@ -115,6 +117,12 @@ def lib() -> C.CDLL:
         "kmws_pipeline_destroy": (None, [vp]),
         "kmws_mask_host_chain": (i32, [vp, vp, vp, sz, i32]),
         "kmws_rx_batch_create": (vp, [i32]),
+        "kmws_tx_batch_create": (vp, [i32]),
+        "kmws_tx_batch_destroy": (None, [vp]),
+        "kmws_tx_batch_add": (i32, [vp, C.POINTER(FrameHdr), vp, vp, sz, vp]),
+        "kmws_tx_batch_flush": (C.c_int64, [vp]),
+        "kmws_tx_batch_pending": (i32, [vp]),
+        "kmws_tx_batch_attach_ring": (i32, [vp, vp, sz]),
         "kmws_rx_batch_destroy": (None, [vp]),
         "kmws_decoder_feed_deferred": (i32, [vp, vp, u8p, sz, FRAME_CB, vp]),
         "kmws_rx_batch_flush": (i32, [vp]),
@@ -130,6 +138,14 @@ def lib() -> C.CDLL:
         fn.restype, fn.argtypes = res, args
     _lib = L
     return L
+
+
+class KmwsError(RuntimeError):
+    """A negative kmws_status from the C ABI (.status)."""
+
+    def __init__(self, status: int, what: str):
+        super().__init__(f"{what} failed with kmws_status {status}")
+        self.status = status
 
 
 def _check(st: int, what: str) -> None:
@@ -289,6 +305,69 @@ class RxBatch:
         try:
             if getattr(self, "_b", None):
                 lib().kmws_rx_batch_destroy(self._b)
+                self._b = None
+        except Exception:
+            pass
+
+
+class TxBatch:
+    """kmws_tx_batch: the send path of many frames masked by one GPU launch per
+    flush (WebSocket::Impl::sendWsFrame, WebSocketImpl.cpp:381-436, batched).
+
+    add(hdr, segments) packs the header now (returned as bytes) and queues the
+    segments -- bytearrays, masked in place at flush -- when hdr.mask is set."""
+
+    def __init__(self, device: int = 0):
+        self._b = lib().kmws_tx_batch_create(device)
+        if not self._b:
+            raise RuntimeError("kmws_tx_batch_create failed (no gfx950 device)")
+        self._keep = []
+
+    def add(self, hdr: "Header", segments) -> bytes:
+        bufs = [(C.c_uint8 * len(x)).from_buffer(x) if len(x) else None for x in segments]
+        ptrs = (C.c_void_p * max(1, len(bufs)))(*[C.cast(b, C.c_void_p) if b is not None else None for b in bufs])
+        lens = (C.c_size_t * max(1, len(bufs)))(*[len(x) for x in segments])
+        out = (C.c_uint8 * MAX_HEADER_SIZE)()
+        h = hdr.to_c()
+        r = lib().kmws_tx_batch_add(self._b, C.byref(h), ptrs, lens, len(bufs), out)
+        self._keep.append((segments, bufs))
+        if r < 0:
+            raise KmwsError(r, "kmws_tx_batch_add")
+        return bytes(out[:r])
+
+    def flush(self) -> int:
+        r = lib().kmws_tx_batch_flush(self._b)
+        self._keep.clear()
+        if r < 0:
+            raise KmwsError(r, "kmws_tx_batch_flush")
+        return r
+
+    def pending(self) -> int:
+        return lib().kmws_tx_batch_pending(self._b)
+
+    def attach_ring(self, ring) -> None:
+        """ring: pinned torch uint8 CPU tensor (kept alive by this object)."""
+        self._ring = ring
+        _check(lib().kmws_tx_batch_attach_ring(self._b, ring.data_ptr() if ring is not None else None,
+                                               ring.numel() if ring is not None else 0),
+               "kmws_tx_batch_attach_ring")
+
+    def add_ptrs(self, hdr: "Header", ptrs, lens) -> bytes:
+        """add() for raw segment addresses (e.g. slices of an attached pinned ring)."""
+        n = len(ptrs)
+        pa = (C.c_void_p * max(1, n))(*ptrs)
+        la = (C.c_size_t * max(1, n))(*lens)
+        out = (C.c_uint8 * MAX_HEADER_SIZE)()
+        h = hdr.to_c()
+        r = lib().kmws_tx_batch_add(self._b, C.byref(h), pa, la, n, out)
+        if r < 0:
+            raise KmwsError(r, "kmws_tx_batch_add")
+        return bytes(out[:r])
+
+    def __del__(self):
+        try:
+            if getattr(self, "_b", None):
+                lib().kmws_tx_batch_destroy(self._b)
                 self._b = None
         except Exception:
             pass

@@ -147,3 +147,13 @@ def test_arena_alloc_without_device_returns_null():
     assert not kmws.lib().kmws_arena_alloc(1 << 20, 0, C.byref(flag))
     assert flag.value == 0
     kmws.lib().kmws_arena_free(None, 0)
+
+
+def test_tx_batch_without_device_is_null():
+    """No gfx950 device here: kmws_tx_batch_create returns NULL (no CPU fallback)."""
+    from kuma_amd import kmws
+    if kmws.lib().kmws_device_count() > 0:
+        pytest.skip("a device is present")
+    assert not kmws.lib().kmws_tx_batch_create(0)
+    with pytest.raises(RuntimeError):
+        kmws.TxBatch()

@@ -2,9 +2,9 @@
 """Secondary measurements for BASELINE.json configs 1, 3, 4 and the
 end-to-end (host-memory) rate.  One JSON line per config on stdout.
 
-  cfg1  1000 x 4 KiB masked TEXT frames, SERVER, fed in 64 KiB reads: the
-        oracle's CPU decoder (kuma's state machine + byte loop) and the
-        product decoder (host parse + GPU unmask), best of N.
+  cfg1  1000 x 4 KiB masked TEXT frames, SERVER, fed in 64 KiB reads (runs
+        bench.py --config cfg1: kuma's decoder restated in oracle/ as the CPU
+        baseline, the product decoder and the batched send path).
   cfg3  Zipf 128 B-1 MiB, ~8 GiB payload, device-resident: encode (header pack
         + mask) -> unpack headers -> gather + unmask; round trip verified.
   cfg4  262,144 messages x 16 x 4 KiB fragments (FIN=0 chains), device-resident:
@@ -40,108 +40,11 @@ def splitmix_keys(seed, n):
 
 # ------------------------------------------------------------------ cfg1
 def cfg1(reps: int):
-    from oracle import oracle as orc
-    from kuma_amd import kmws
-    n, L = 1000, 4096
-    rng = np.random.default_rng(SEED)
-    keys = splitmix_keys(SEED, n)
-    payload = (0x20 + rng.integers(0, 2**31, size=n * L) % 95).astype(np.uint8)
-    src_off = np.arange(n, dtype=np.uint64) * L
-    flags = np.full(n, 0x81 | 0x100, dtype=np.uint32)
-    wire, _ = orc.encode_batch(payload, src_off, np.full(n, L), flags, keys)
-    wire = bytes(wire)
-    chunk = 64 * 1024
-
-    # Every decoder / batch is long-lived, as on an event loop (one per
-    # connection / loop thread): created once, warmed by one untimed pass (its
-    # pinned staging grows to size), then the best of `reps` timed passes.
-    def run(create, feed, destroy):
-        d = create()
-        bufs = [bytearray(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
-        cbufs = [(C.c_uint8 * len(b)).from_buffer(b) for b in bufs]
-        best = 1e9
-        for rep in range(reps + 1):
-            for i, b in enumerate(bufs):  # fresh masked bytes (the decoder unmasks in place)
-                b[:] = wire[i * chunk:i * chunk + len(b)]
-            t0 = time.perf_counter()
-            for b, cb in zip(bufs, cbufs):
-                r = feed(d, cb, len(b))
-                assert r in (0, 1), r
-            if rep:
-                best = min(best, time.perf_counter() - t0)
-        destroy(d)
-        return best
-
-    O = orc.lib()
-    t_orc = run(lambda: O.orc_decoder_create(1),
-                lambda d, b, l: O.orc_decoder_feed(d, b, l, C.cast(None, orc.FRAME_CB), None),
-                O.orc_decoder_destroy)
-    res = {"config": "cfg1", "frames": n, "frame_len": L, "wire_bytes": len(wire), "feed_chunk": chunk,
-           "oracle_cpu": {"GiB_s": n * L / t_orc / 2**30, "us_per_frame": t_orc / n * 1e6, "threads": 1,
-                          "best_of": reps}}
-    if kmws.device_count() > 0:
-        K = kmws.lib()
-        t_gpu = run(lambda: K.kmws_decoder_create(1, 0),
-                    lambda d, b, l: K.kmws_decoder_feed(d, b, l, C.cast(None, kmws.FRAME_CB), None),
-                    K.kmws_decoder_destroy)
-        res["product_decoder_sync"] = {"GiB_s": n * L / t_gpu / 2**30, "us_per_frame": t_gpu / n * 1e6,
-                                       "best_of": reps,
-                                       "note": "kmws_decoder_feed: host parse + one GPU unmask per 64 KiB read "
-                                               "(pageable chunk -> pinned staging, zero-copy kernel); bounded "
-                                               "below by one HIP launch + stream sync per read"}
-        # deferred: every read of the burst fed, ONE flush (one GPU batch per loop iteration)
-        nullcb = C.cast(None, kmws.FRAME_CB)
-        bufs = [bytes(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]
-        cbufs = [(C.c_uint8 * len(x)).from_buffer_copy(x) for x in bufs]
-        d = K.kmws_decoder_create(1, 0)
-        b = K.kmws_rx_batch_create(0)
-        best = 1e9
-        for rep in range(reps + 1):
-            t0 = time.perf_counter()
-            for x, cb in zip(bufs, cbufs):
-                r = K.kmws_decoder_feed_deferred(d, b, cb, len(x), nullcb, None)
-                assert r in (0, 1), r
-            got = K.kmws_rx_batch_flush(b)
-            if rep:
-                best = min(best, time.perf_counter() - t0)
-            assert got == n, got
-        K.kmws_rx_batch_destroy(b)
-        K.kmws_decoder_destroy(d)
-        res["product_decoder_deferred"] = {"GiB_s": n * L / best / 2**30, "us_per_frame": best / n * 1e6,
-                                           "best_of": reps,
-                                           "note": "kmws_decoder_feed_deferred per read + one kmws_rx_batch_flush"}
-        # deferred + pinned receive ring: reads land in the ring (recv into the ring replaces
-        # kuma's recv into a stack buffer, untimed here as in the CPU case), zero-copy unmask
-        import torch
-        ring = torch.empty(len(wire) + 64 * 128, dtype=torch.uint8).pin_memory()
-        wire_t = torch.frombuffer(bytearray(wire), dtype=torch.uint8)
-        d = K.kmws_decoder_create(1, 0)
-        b = K.kmws_rx_batch_create(0)
-        assert K.kmws_rx_batch_attach_ring(b, ring.data_ptr(), ring.numel()) == 0
-        best = 1e9
-        for rep in range(reps + 1):
-            offs = []
-            w = 0
-            for i in range(0, len(wire), chunk):
-                m = min(chunk, len(wire) - i)
-                ring[w:w + m] = wire_t[i:i + m]
-                offs.append((w, m))
-                w += m + 64  # reads land at arbitrary ring positions
-            base = ring.data_ptr()
-            t0 = time.perf_counter()
-            for o, m in offs:
-                r = K.kmws_decoder_feed_deferred(d, b, base + o, m, nullcb, None)
-                assert r in (0, 1), r
-            got = K.kmws_rx_batch_flush(b)
-            if rep:
-                best = min(best, time.perf_counter() - t0)
-            assert got == n, got
-        K.kmws_rx_batch_destroy(b)
-        K.kmws_decoder_destroy(d)
-        res["product_decoder_deferred_ring"] = {"GiB_s": n * L / best / 2**30, "us_per_frame": best / n * 1e6,
-                                                "best_of": reps,
-                                                "note": "reads in a pinned ring attached to the batch; one flush"}
-    return res
+    """BASELINE configs[0]: lives in bench.py (`python bench.py --config cfg1`),
+    whose cpu_baseline leg times kuma's decoder restated in oracle/."""
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.run_cfg1(reps)
 
 
 # ------------------------------------------------------------------ cfg3

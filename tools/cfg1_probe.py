@@ -1,7 +1,9 @@
 """Where the synchronous decoder's time per 64 KiB read goes (cfg1 shape):
 feed of a chunk of 16 x 4 KiB UNMASKED frames (host parse only, no GPU) vs
 MASKED frames (parse + staging + one GPU launch + wait + write-back), pageable
-vs pinned chunk; plus memcpy into pinned memory and a bare torch launch+sync."""
+vs pinned chunk; plus memcpy into pinned memory and a bare torch launch+sync.
+(The CPU decoder's time for the same read is bench.py --config cfg1's
+cpu_baseline; profiles/r01i_cfg1_latency.txt has both.)"""
 import ctypes as C
 import os
 import sys
@@ -15,18 +17,27 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     import torch
     from kuma_amd import kmws
-    from oracle import oracle as orc
     K = kmws.lib()
     n, L = 16, 4096
     rng = np.random.default_rng(1)
     payload = rng.integers(0, 256, size=n * L, dtype=np.uint8)
     keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
-    offs = np.arange(n, dtype=np.uint64) * L
+
+    def frames_wire(mask):
+        """n x 4 KiB BINARY frames: 82 fe 10 00 [key] payload(^key)."""
+        out = bytearray()
+        for i in range(n):
+            k = int(keys[i]).to_bytes(4, "little")
+            p = payload[i * L:(i + 1) * L]
+            out += bytes([0x82, (0x80 if mask else 0) | 126, L >> 8, L & 0xFF])
+            if mask:
+                out += k
+                p = p ^ np.tile(np.frombuffer(k, dtype=np.uint8), L // 4)
+            out += p.tobytes()
+        return bytes(out)
     res = {}
     for name, mask in (("unmasked", 0), ("masked", 1)):
-        flags = np.full(n, 0x82 | (mask << 8), dtype=np.uint32)
-        wire, _ = orc.encode_batch(payload, offs, np.full(n, L), flags, keys)
-        wire = bytes(wire)
+        wire = frames_wire(mask)
         for mem in ("pageable", "pinned"):
             mode = 1 if mask else 0  # SERVER needs masked frames, CLIENT unmasked
             d = K.kmws_decoder_create(mode, 0)
@@ -49,21 +60,7 @@ def main():
                 assert r == 0, r
             K.kmws_decoder_destroy(d)
             res[f"{name}_{mem}_us"] = round(float(np.median(ts[50:])) * 1e6, 2)
-    # orc decoder, same masked chunk
-    flags = np.full(n, 0x82 | 0x100, dtype=np.uint32)
-    wire, _ = orc.encode_batch(payload, offs, np.full(n, L), flags, keys)
-    wire = bytes(wire)
-    O = orc.lib()
-    d = O.orc_decoder_create(1)
-    b = bytearray(wire)
-    ptr = (C.c_uint8 * len(b)).from_buffer(b)
-    ts = []
-    for i in range(300):
-        b[:] = wire
-        t0 = time.perf_counter()
-        O.orc_decoder_feed(d, ptr, len(b), C.cast(None, orc.FRAME_CB), None)
-        ts.append(time.perf_counter() - t0)
-    res["oracle_masked_us"] = round(float(np.median(ts[50:])) * 1e6, 2)
+    wire = frames_wire(1)
     # memcpy 64 KiB into pinned memory, bare launch + sync
     pin = torch.empty(1 << 16, dtype=torch.uint8).pin_memory()
     srcn = np.frombuffer(wire[:1 << 16], dtype=np.uint8)
