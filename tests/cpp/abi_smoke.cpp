@@ -80,8 +80,27 @@ int main()
         const uint8_t k[4] = {1, 2, 3, 4};
         CHECK(kmws_mask_host_chain(k, segs, lens, 2, 0) == KMWS_OK);  // SURVEY a-2 vector
         CHECK(hex(seg1, 3) == "010203" && hex(seg2, 5) == "0401020304");
+        // batched send path: RFC 6455 5.7 masked "Hello" built from two segments, one flush
+        kmws_tx_batch* tx = kmws_tx_batch_create(0);
+        CHECK(tx != nullptr);
+        uint8_t he[2] = {'H', 'e'}, llo[3] = {'l', 'l', 'o'};
+        uint8_t* tsegs[2] = {he, llo};
+        size_t tlens[2] = {2, 3};
+        kmws_frame_hdr th;
+        std::memset(&th, 0, sizeof th);
+        th.fin = 1;
+        th.opcode = KMWS_OP_TEXT;
+        th.mask = 1;
+        const uint8_t tk[4] = {0x37, 0xfa, 0x21, 0x3d};
+        std::memcpy(th.maskey, tk, 4);
+        uint8_t hb[KMWS_MAX_HEADER_SIZE];
+        CHECK(kmws_tx_batch_add(tx, &th, tsegs, tlens, 2, hb) == 6 && hex(hb, 6) == "818537fa213d");
+        CHECK(kmws_tx_batch_pending(tx) == 1 && kmws_tx_batch_flush(tx) == 1);
+        CHECK(hex(he, 2) == "7f9f" && hex(llo, 3) == "4d5158");
+        kmws_tx_batch_destroy(tx);
     } else {
         CHECK(r == KMWS_ERR_NOT_SUPPORTED && g3.payloads.empty());
+        CHECK(kmws_tx_batch_create(0) == nullptr);
     }
     kmws_decoder_destroy(srv);
     std::printf("%s (%d failures)\n", fails ? "FAILED" : "OK", fails);
