@@ -3,6 +3,7 @@ kmws_encode_batch (header pack + masked payload), kmws_unpack_headers
 (descriptor-indexed header decode/validation), kmws_gather_unmask, and the
 encode -> find headers -> unpack -> unmask round trip."""
 import json
+import zlib
 import os
 
 import numpy as np
@@ -90,7 +91,7 @@ def gpu_encode(T, src, offs, lens, flags, keys, cap=None):
 @pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k", "max"])
 @pytest.mark.parametrize("aligned", [True, False])
 def test_encode_parity(T, kind, aligned):
-    rng = np.random.default_rng(abs(hash((kind, aligned))) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(f"{kind}-{aligned}".encode()))
     n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6}[kind]
     lens, flags, keys = frames(rng, kind, n)
     src, offs = src_arena(rng, lens, aligned)
@@ -127,7 +128,7 @@ def wire_and_offsets(rng, kind, n, mode_mask=1):
 @pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max"])
 def test_unpack_gather_roundtrip(T, kind):
     from kuma_amd import kmws
-    rng = np.random.default_rng(abs(hash(kind)) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(str(kind).encode()))
     wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, kind, 250 if kind != "max" else 6)
     hdr, used = kmws.find_headers(bytes(wire))
     # CLOSE frames stop the reference parser: cut the batch there like it does

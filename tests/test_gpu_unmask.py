@@ -4,6 +4,8 @@ Every case builds a host buffer + descriptors, unmasks a copy with the oracle
 (WSHandler.cpp:303-310 byte loop, restated in oracle/kmws_oracle.c) and the
 other copy on the GPU through the C ABI, and compares every byte of the
 buffer (payload, headers, gaps)."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -95,7 +97,7 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 66, 65537, 2097152])
 def test_unmask_parity(torch_dev, kind, variant):
-    rng = np.random.default_rng(abs(hash((kind, variant))) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(f"{kind}-{variant}".encode()))
     buf, descs = layout(kind, rng)
     want = buf.copy()
     orc.unmask_batch(want, descs)

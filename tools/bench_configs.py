@@ -147,20 +147,30 @@ def cfg3(reps: int, gib: float):
             "note": "decode is descriptor-indexed: header offsets = the receiver's host parse (here wire_off)"}
 
 
-def pinned_host(torch, nbytes: int):
+class PinnedHost:
     """Exactly nbytes of page-locked host memory: numpy pages (touched, so they
     are resident) registered with hipHostRegister.  torch's pin_memory() would
     round the request up to a power of two in its caching host allocator (two
-    8 GiB buffers become 32 GiB pinned), and the copy engines ran at a third of
-    the PCIe rate over such large pinned sets."""
-    a = np.empty(nbytes, dtype=np.uint8)
-    a.fill(0)
-    rt = torch.cuda.cudart()
-    if int(rt.cudaHostRegister(a.ctypes.data, nbytes, 0)) != 0:
-        raise RuntimeError("hipHostRegister failed")
-    t = torch.from_numpy(a)
-    assert t.is_pinned()
-    return t, a
+    8 GiB buffers become 32 GiB pinned).  close() unregisters BEFORE the numpy
+    pages are released: a registration outliving its pages would make the
+    runtime treat a later allocation at the same addresses as pinned and DMA
+    through the stale mapping (an illegal-address fault on the next H2D copy)."""
+
+    def __init__(self, torch, nbytes: int):
+        self._rt = torch.cuda.cudart()
+        self.array = np.empty(nbytes, dtype=np.uint8)
+        self.array.fill(0)
+        if int(self._rt.cudaHostRegister(self.array.ctypes.data, nbytes, 0)) != 0:
+            raise RuntimeError("hipHostRegister failed")
+        self.tensor = torch.from_numpy(self.array)
+        assert self.tensor.is_pinned()
+
+    def close(self):
+        if self.array is not None:
+            self.tensor = None
+            if int(self._rt.cudaHostUnregister(self.array.ctypes.data)) != 0:
+                raise RuntimeError("hipHostUnregister failed")
+            self.array = None
 
 
 def cfg3_e2e(gib: float, chunk_mib: int, reps: int):
@@ -195,9 +205,20 @@ def cfg3_e2e(gib: float, chunk_mib: int, reps: int):
         h0 = int(pay_off[a]) & ~15
         rel[a:b] = pay_off[a:b] - h0
         chunks.append((a, b, h0, int(pay_off[b]) - h0, int(pay_off[b] - pay_off[a]), int((hl[a:b] + lens[a:b]).sum())))
+    torch.cuda.synchronize()
+    pin_src, pin_dst = PinnedHost(torch, P + 32), PinnedHost(torch, P + 32)
+    try:
+        return _cfg3_e2e_run(torch, kmws, pin_src.tensor, pin_dst.tensor, P, n, lens, pay_off, rel, flags, keys,
+                             chunks, cb, chunk_mib, reps)
+    finally:
+        torch.cuda.synchronize()  # no copy still reading or writing the pages
+        pin_src.close()
+        pin_dst.close()
+
+
+def _cfg3_e2e_run(torch, kmws, host_src, host_dst, P, n, lens, pay_off, rel, flags, keys, chunks, cb, chunk_mib,
+                  reps):
     dev = torch.device("cuda")
-    host_src, _keep_src = pinned_host(torch, P + 32)
-    host_dst, _keep_dst = pinned_host(torch, P + 32)
     tmp = torch.empty(P + 32, dtype=torch.uint8, device=dev)
     kmws.fill_synthetic(tmp, SEED ^ 9)
     host_src.copy_(tmp)
