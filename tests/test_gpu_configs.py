@@ -2,6 +2,8 @@
 pipeline at reduced sizes, through tools/bench_configs.py (the same code that
 produces the measured numbers), verified on the device:
 
+  cfg2b 64 KiB frames as a packed wire (14-byte headers, misaligned
+        payloads) unmasked in place: every byte checked on the device;
   cfg3  Zipf 128 B - 1 MiB frames: encode (header pack + mask) -> unpack
         headers -> gather + unmask; every payload byte equals the source
         (index-gather check independent of the kernels);
@@ -53,3 +55,8 @@ def test_e2e_pipeline_roundtrip(bc):
 def test_cfg3_e2e_roundtrip(bc):
     r = bc.cfg3_e2e(0.25, 8, 1)  # 8 MiB chunks: ~32 chunks, every slot reused many times
     assert r["verified"] and r["chunks"] > 6
+
+
+def test_cfg2b_packed_wire(bc):
+    r = bc.cfg2b(2, 8192)  # 512 MiB: beyond the MALL, boundary tiles on the general path
+    assert r["verified"]

@@ -298,6 +298,35 @@ def _cfg3_e2e_run(torch, kmws, host_src, host_dst, P, n, lens, pay_off, rel, fla
                     "3 slots on 3 streams; PCIe-bound (each payload byte crosses twice)"}
 
 
+def cfg2b(reps: int, frames: int):
+    """BASELINE configs[1] variant B (SURVEY 8 d row 2): the same 1 M x 64 KiB
+    frames as a packed wire image -- 14-byte masked headers between payloads,
+    so payload starts are misaligned (payload f at 14 + f * 65,550) -- unmasked
+    in place on the device.  Tiles holding a frame boundary take the general
+    (descriptor-staged, byte-exact) path; headers keep their bytes."""
+    import torch
+    from kuma_amd import kmws
+    L, H = 65536, 14
+    n = frames
+    span = n * (L + H)
+    dev = torch.device("cuda")
+    wire = torch.empty(span, dtype=torch.uint8, device=dev)
+    kmws.fill_synthetic(wire, SEED)
+    descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    kmws.fill_uniform_descs(descs, L + H, L, SEED ^ 7)
+    descs[:, 0] += H
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span))
+    sched = kmws.unmask_autotune(wire, descs, ws, span)
+    kmws.unmask_batch(wire, descs, ws, span)  # odd number of passes in total: verify the masked state
+    t = timed(torch, lambda: kmws.unmask_batch(wire, descs, ws, span), 2 * (reps // 2) + 2)  # even: back to masked
+    ok = ws.status() == 0 and kmws.check_unmasked(wire, SEED, descs) == 0
+    alg = n * (2 * L + 16)
+    return {"config": "cfg2b", "frames": n, "frame_len": L, "header_len": H, "span_bytes": span,
+            "schedule": sched, "ms": t * 1e3, "payload_GiB_s": n * L / t / 2**30,
+            "alg_GB_s": alg / t / 1e9, "hbm_frac": alg / t / 8e12, "verified": bool(ok),
+            "note": "device-resident packed wire (14-B headers, misaligned payloads), in-place unmask, plan + apply"}
+
+
 # ------------------------------------------------------------------ cfg4
 def cfg4(reps: int, messages: int):
     import torch
@@ -393,7 +422,8 @@ def e2e(gib: float, chunk_mib: int, depth: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
+    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
+    ap.add_argument("--cfg2b-frames", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cfg3-gib", type=float, default=8.0)
     ap.add_argument("--cfg4-messages", type=int, default=262144)
@@ -404,6 +434,8 @@ def main():
     for w in a.which:
         if w == "cfg1":
             r = cfg1(max(a.reps, 10))
+        elif w == "cfg2b":
+            r = cfg2b(a.reps, a.cfg2b_frames)
         elif w == "cfg3":
             r = cfg3(a.reps, a.cfg3_gib)
         elif w == "cfg3_e2e":
