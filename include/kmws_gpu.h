@@ -8,13 +8,20 @@
  * kmws_status (0 = OK, negative = kuma KMError value, include/kmdefs.h:61-86)
  * unless noted; codec results use kuma's WSError numbering (wsdefs.h:56-67).
  *
- * Two families:
+ * Three families:
  *  - host codec entries (kmws_encode_header, kmws_decoder_*): the per-connection,
  *    byte-stream state machine that kuma runs on its event-loop thread.  The
  *    decoder parses headers on the host; payload unmasking is done by the GPU
  *    kernels below (batched per feed call).  See DESIGN.md "Boundary".
- *  - device batch entries (kmws_*_batch): stream-ordered, no host sync, no
- *    allocation; all pointers are device pointers; workspace is caller-owned.
+ *  - loop-level host batches: kmws_rx_batch_* (receive: one GPU batch per
+ *    event-loop iteration across reads and connections), kmws_tx_batch_*
+ *    (send: one GPU mask launch for every send of an iteration),
+ *    kmws_mask_host_chain and kmws_pipeline_* (host-resident frame batches);
+ *    synchronous, pinned staging or zero-copy on caller-pinned memory.
+ *  - device batch entries (kmws_*_batch, kmws_unpack_headers,
+ *    kmws_gather_unmask): stream-ordered, no host sync, no allocation; all
+ *    pointers are device pointers; workspace is caller-owned.  Set-up helpers
+ *    (kmws_unmask_autotune, kmws_arena_*) may synchronize and allocate.
  */
 #ifndef KMWS_GPU_H
 #define KMWS_GPU_H
