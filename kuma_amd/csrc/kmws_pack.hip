@@ -572,12 +572,15 @@ __device__ __forceinline__ void edge_block(uint64_t blk, const uint8_t* __restri
     edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, g, fl, src, start, d, flags);
 }
 
+#ifndef KMWS_REC_EDGE_WAVES
+#define KMWS_REC_EDGE_WAVES 1  // min waves per SIMD the register budget must allow (tuning)
+#endif
 // Unit records and edge words in one grid (they are independent, and the
 // record blocks alone are too few to fill the chip): virtual block v < rec_blocks
 // writes records, v >= rec_blocks composes edge words (edge block v - rec_blocks);
 // v = vbase + blockIdx.x, the grid being cut at 2^31 work-items per launch.
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) rec_edge_kernel(const uint8_t* __restrict__ src,
+__global__ void __launch_bounds__(kBlock, KMWS_REC_EDGE_WAVES) rec_edge_kernel(const uint8_t* __restrict__ src,
                                                           const uint64_t* __restrict__ start,
                                                           const uint64_t* __restrict__ ubase,
                                                           const kmws_desc* __restrict__ d,
