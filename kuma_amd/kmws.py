@@ -550,16 +550,26 @@ def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
                                     _stream_handle(stream)), "kmws_gather_unmask")
 
 
-def find_headers(wire: bytes, cap: Optional[int] = None):
+def find_headers_into(buf, out) -> tuple:
+    """kmws_find_headers over a uint8 numpy array into a preallocated uint64
+    numpy array (no copies): -> (headers found, consumed bytes)."""
+    n, used = C.c_uint32(0), C.c_uint64(0)
+    _check(lib().kmws_find_headers(buf.ctypes.data, buf.nbytes, out.ctypes.data, len(out), C.byref(n),
+                                   C.byref(used)), "kmws_find_headers")
+    return n.value, used.value
+
+
+def find_headers(wire, cap: Optional[int] = None):
     """Host header-chain walk -> (list of header offsets, consumed bytes)."""
     import numpy as np
-    buf = np.frombuffer(bytes(wire), dtype=np.uint8) if len(wire) else np.zeros(1, np.uint8)
-    cap = len(wire) // 2 + 1 if cap is None else cap
+    if isinstance(wire, np.ndarray):
+        buf = wire
+    else:
+        buf = np.frombuffer(bytes(wire), dtype=np.uint8) if len(wire) else np.zeros(0, np.uint8)
+    cap = buf.nbytes // 2 + 1 if cap is None else cap
     out = np.zeros(max(1, cap), dtype=np.uint64)
-    n, used = C.c_uint32(0), C.c_uint64(0)
-    _check(lib().kmws_find_headers(buf.ctypes.data, len(wire), out.ctypes.data, cap, C.byref(n),
-                                   C.byref(used)), "kmws_find_headers")
-    return out[:n.value].tolist(), used.value
+    n, used = find_headers_into(buf, out[:cap] if cap else out[:1])
+    return out[:n].tolist(), used
 
 
 class Pipeline:

@@ -366,9 +366,13 @@ def cfg4(reps: int, messages: int):
     t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), reps)
     # host boundary discovery rate (the serial part a receiver runs as bytes arrive), 1 GiB sample
     sample = wire[:min(P + H, 1 << 30)].cpu().numpy()
-    t0 = time.perf_counter()
-    hdrs, _ = kmws.find_headers(sample.tobytes())
-    t_walk = time.perf_counter() - t0
+    out = np.zeros(sample.nbytes // 2 + 1, dtype=np.uint64)
+    t_walk = 1e9
+    for _ in range(3):  # the C walk only (no copies, no list conversion), best of 3
+        t0 = time.perf_counter()
+        nh, _ = kmws.find_headers_into(sample, out)
+        t_walk = min(t_walk, time.perf_counter() - t0)
+    hdrs = out[:nh]
     return {"config": "cfg4", "messages": messages, "frames": n, "payload_bytes": P,
             "pack": {"ms": t_pack * 1e3, "Mheaders_s": n / t_pack / 1e6, "payload_GiB_s": P / t_pack / 2**30,
                      "hbm_frac": (2 * P + H + 26 * n) / t_pack / 8e12},
