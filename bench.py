@@ -337,6 +337,14 @@ def run_cfg1(reps: int = 10) -> dict:
 PLACEMENT_STEP = 16 << 30
 
 
+def placement_slack(span: int, free: int, want: int) -> int:
+    """Arena bytes beyond the batch for the placement probe: a multiple of
+    16 GiB, at most `want`, at most 1.5 x the batch, and what fits beside the
+    batch in free memory with 8 GiB to spare (< 16 GiB: no probe)."""
+    st = PLACEMENT_STEP
+    return max(0, min(want, span * 3 // 2 // st * st, (free - span - (8 << 30)) // st * st))
+
+
 def place_batch(kmws, torch, dev, span, slack):
     """Carves the batch out of one physically contiguous arena of span + slack
     bytes, at the offset (multiples of 16 GiB) where two in-place split-8 unmask
@@ -346,7 +354,7 @@ def place_batch(kmws, torch, dev, span, slack):
     see physical addresses, so the layout is chosen by measurement once, as a
     long-lived batch ring would be.  Returns (arena | None, batch view, record)."""
     free, _ = torch.cuda.mem_get_info(dev)
-    slack = min(slack, span * 3 // 2 // PLACEMENT_STEP * PLACEMENT_STEP, (free - span - (8 << 30)) // PLACEMENT_STEP * PLACEMENT_STEP)
+    slack = placement_slack(span, free, slack)
     if slack < PLACEMENT_STEP:
         return None, None, {"kind": "plain torch.empty", "why": "no room for a placement probe"}
     try:

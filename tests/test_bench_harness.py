@@ -1,0 +1,80 @@
+"""CPU checks of bench.py's harness pieces (no GPU): the cfg1 wire image the
+benchmark feeds is a valid masked stream that kuma's decoder (oracle)
+decodes back to the plain payloads, and the placement/sub-batch arithmetic
+the headline run relies on."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+from kuma_amd import shard
+from oracle import oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_cfg1_cpu_baseline_runs_without_gpu():
+    """bench.py --config cfg1 on a host without a GPU: the cpu_baseline leg
+    (kuma's decoder restated in oracle/) decodes the whole stream; no product
+    numbers are reported (no CPU fallback)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg1", "--steps", "2"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"] == "cfg1" and d["frames"] == 1000 and d["wire_bytes"] == 1000 * (8 + 4096)
+    assert d["cpu_baseline"]["GiB_s"] > 0 and d["cpu_baseline"]["cores"] == 1
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if not has_gpu:
+        assert not any(k.startswith("product") for k in d)
+
+
+def test_cfg1_wire_decodes_to_plain_payloads():
+    """The wire construction used by bench.run_cfg1 (81 fe 10 00 key | payload ^ key)
+    equals the oracle's encodeFrameHeader + mask for every frame."""
+    n, L = 8, 4096
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    payload = (0x20 + rng.integers(0, 95, size=n * L)).astype(np.uint8)
+    kb = keys.view(np.uint8).reshape(n, 4)
+    frames = np.empty((n, 8 + L), dtype=np.uint8)
+    frames[:, :4] = np.array([0x81, 0xFE, L >> 8, L & 0xFF], dtype=np.uint8)
+    frames[:, 4:8] = kb
+    frames[:, 8:] = payload.reshape(n, L) ^ np.tile(kb, L // 4)
+    want = b"".join(orc.encode_header(orc.Hdr(fin=1, opcode=1, mask=1, maskey=bytes(kb[i]), length=L)) +
+                    orc.mask_bytes(bytes(kb[i]), payload[i * L:(i + 1) * L].tobytes()) for i in range(n))
+    assert frames.tobytes() == want
+    rets, fr = orc.decode_chunks(want, orc.SERVER, 65536)
+    assert rets[-1] == 0 and [f.payload for f in fr] == [payload[i * L:(i + 1) * L].tobytes() for i in range(n)]
+
+
+def test_placement_slack_and_offsets():
+    """place_batch's slack rule: multiples of 16 GiB, at most 1.5 x the batch and
+    what fits beside it; offsets 0, 16, ... GiB inside the arena."""
+    sys.path.insert(0, ROOT)
+    import bench
+    step = bench.PLACEMENT_STEP
+    assert step == 16 << 30
+
+    def slack(span, free, want=96 << 30):
+        return bench.placement_slack(span, free, want)
+
+    assert slack(64 << 30, 280 << 30) == 96 << 30            # cfg2 on a 288 GB GPU: 160 GiB arena
+    assert slack(80 << 30, 280 << 30) == 96 << 30            # cfg5 resident batch: 176 GiB arena
+    assert slack(16 << 30, 280 << 30) == 16 << 30            # small batches: little slack
+    assert slack(4 << 30, 280 << 30) < step                  # too small to probe: plain allocation
+    assert slack(64 << 30, 100 << 30) == 16 << 30            # memory already in use: what fits
+    assert slack(64 << 30, 60 << 30) == 0                    # not even the batch fits beside: no probe
+    offsets = list(range(0, (96 << 30) + 1, step))
+    assert len(offsets) == 7 and offsets[-1] + (64 << 30) == 160 << 30
+
+
+def test_cfg5_sub_batches_per_gpu_count():
+    for world, nb in ((1, 8), (2, 4), (4, 2), (8, 1)):
+        n, bs = shard.sub_batches(10485760, 0, world, 1310720)
+        assert len(bs) == nb and n == 1310720
