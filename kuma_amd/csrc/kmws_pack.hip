@@ -781,7 +781,18 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
 }
 
 // ------------------------------ header unpack / validate ------------------------------
+// Byte k (0..15) of a 16-byte register word.
+__device__ __forceinline__ uint32_t byte_of(const u32x4& v, uint32_t k)
+{
+    const uint32_t q = k >> 2;
+    const uint32_t w = (q & 2u) ? ((q & 1u) ? v.w : v.z) : ((q & 1u) ? v.y : v.x);
+    return (w >> (8u * (k & 3u))) & 0xFFu;
+}
+
 // One lane per frame: the reference's HDR1..MASKEY rules (WSHandler.cpp:118-234).
+// The (at most 14) header bytes come from ONE pair of aligned 16-byte loads,
+// funnel-shifted into a register word, when both words lie inside the wire;
+// headers within 32 bytes of its end are read byte by byte (same rules).
 __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                                 const uint64_t* __restrict__ hdr_off, uint32_t n,
                                                                 int mode, kmws_desc* __restrict__ out_desc,
@@ -793,14 +804,36 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
     if (f >= n) return;
     const uint64_t h = hdr_off[f];
     const uint64_t limit = f + 1 < n ? hdr_off[f + 1] : wire_len;  // this frame must end by the next header
+    // the header window: bytes h .. h + 15 that lie inside the wire (avail of them)
+    const uint64_t avail = h < wire_len ? (wire_len - h < 16 ? wire_len - h : 16) : 0;
+    u32x4 hw = u32x4{0, 0, 0, 0};
+    // aligned 16-byte words by absolute address: a word holding any wire byte is
+    // readable (it cannot cross a page), whatever the wire's own alignment
+    const uintptr_t a = reinterpret_cast<uintptr_t>(wire + h);
+    const uintptr_t a16 = a & ~(uintptr_t)15;
+    const uintptr_t end16 = (reinterpret_cast<uintptr_t>(wire) + wire_len + 15) & ~(uintptr_t)15;
+    if (h < wire_len && a16 + 32 <= end16) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(a16);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(a16 + 16);
+        hw = funnel16(lo, hi, (uint32_t)(a & 15u));
+    } else {
+        for (uint32_t k = 0; k < (uint32_t)avail; ++k) {
+            const uint32_t b = wire[h + k];
+            const uint32_t sh = 8u * (k & 3u);
+            if ((k >> 2) == 0) hw.x |= b << sh;
+            else if ((k >> 2) == 1) hw.y |= b << sh;
+            else if ((k >> 2) == 2) hw.z |= b << sh;
+            else hw.w |= b << sh;
+        }
+    }
     uint8_t err = KMWS_WS_NOERR;
     uint32_t len = 0, key = 0, hl = 2;
     uint32_t b0 = 0, b1 = 0;
     if (h + 2 > wire_len || limit < h || limit > wire_len) {
         err = h + 2 > wire_len ? KMWS_WS_NEED_MORE_DATA : KMWS_WS_INVALID_FRAME;
     } else {
-        b0 = wire[h];
-        b1 = wire[h + 1];
+        b0 = hw.x & 0xFFu;
+        b1 = (hw.x >> 8) & 0xFFu;
         const uint32_t fin = b0 >> 7, op = b0 & 0x0F, mask = b1 >> 7, plen = b1 & 0x7F;
         if (!fin && op >= 8) {
             err = KMWS_WS_PROTOCOL_ERROR;                     // :126-130
@@ -812,13 +845,14 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
             if (h + 2 + ext > wire_len) {
                 err = KMWS_WS_NEED_MORE_DATA;
             } else if (plen == 126) {                          // :159-175
-                len = ((uint32_t)wire[h + 2] << 8) | wire[h + 3];
+                len = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
                 if (len < 126) err = KMWS_WS_INVALID_LENGTH;
             } else if (plen == 127) {                          // :176-197, x86-64 shift quirk
                 uint64_t x = 0;
+#pragma unroll
                 for (uint32_t k = 0; k < 8; ++k) {
                     const uint32_t sh = ((7u - k) * 8u) & 31u;
-                    x |= (uint64_t)(int64_t)(int32_t)((uint32_t)wire[h + 2 + k] << sh);
+                    x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << sh);
                 }
                 if ((x >> 63) != 0) err = KMWS_WS_INVALID_LENGTH;
                 else {
@@ -832,9 +866,10 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
                 if (mask && mode == KMWS_MODE_CLIENT) err = KMWS_WS_PROTOCOL_ERROR;          // :208-212
                 else if (!mask && mode == KMWS_MODE_SERVER && len > 0) err = KMWS_WS_PROTOCOL_ERROR;  // :225-229
                 else if (h + hl > wire_len) err = KMWS_WS_NEED_MORE_DATA;
-                else if (mask) {
-                    key = (uint32_t)wire[h + hl - 4] | ((uint32_t)wire[h + hl - 3] << 8) |
-                          ((uint32_t)wire[h + hl - 2] << 16) | ((uint32_t)wire[h + hl - 1] << 24);
+                else if (mask) {  // key bytes verbatim at hl - 4 (2, 4 or 10)
+                    const uint32_t k0 = hl - 4;
+                    key = byte_of(hw, k0) | (byte_of(hw, k0 + 1) << 8) | (byte_of(hw, k0 + 2) << 16) |
+                          (byte_of(hw, k0 + 3) << 24);
                 }
                 if (err == KMWS_WS_NOERR) {
                     if (h + hl + len > wire_len) err = KMWS_WS_NEED_MORE_DATA;

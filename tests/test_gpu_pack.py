@@ -143,6 +143,14 @@ def test_unpack_gather_roundtrip(T, kind):
     kmws.unpack_headers(d_wire, d_hdr, kmws.SERVER, out_desc, out_flags, out_err, ws, wire_len=len(wire))
     T.cuda.synchronize()
     assert ws.status() == 0 and (out_err.cpu().numpy() == 0).all()
+    for shift in (1, 7, 15):  # the same wire at unaligned addresses: identical descriptors (offsets relative)
+        u = T.zeros(len(wire) + 64, dtype=T.uint8, device="cuda")
+        u[shift:shift + len(wire)] = d_wire[:len(wire)]
+        od2 = T.zeros((n, 2), dtype=T.int64, device="cuda")
+        oe2 = T.full((n,), 99, dtype=T.uint8, device="cuda")
+        kmws.unpack_headers(u[shift:shift + len(wire)], d_hdr, kmws.SERVER, od2, None, oe2, ws, wire_len=len(wire))
+        T.cuda.synchronize()
+        assert T.equal(od2, out_desc) and T.equal(oe2, out_err), shift
     dd = out_desc.cpu().numpy().view(orc.DESC_DTYPE).reshape(-1)
     # oracle decode of the same stream (SERVER) gives the frames
     rets, ofr = orc.decode_chunks(bytes(wire[:used]), orc.SERVER, 0)
