@@ -32,6 +32,22 @@ __global__ void xor_once(u32x4* buf, uint32_t words)
         buf[w] ^= u32x4{0x01020304u, 0x05060708u, 0x090a0b0cu, 0x0d0e0f10u};
 }
 
+// (c) one launch per job whose last block raises a completion flag in host memory;
+// the host spins on the flag instead of hipStreamSynchronize.
+__global__ void xor_flag(u32x4* buf, uint32_t words, unsigned int* counter, uint64_t* flag, uint64_t seq)
+{
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < words; w += gridDim.x * blockDim.x) {
+        u32x4 v = __builtin_nontemporal_load(buf + w);
+        __builtin_nontemporal_store(v ^ u32x4{0x01020304u, 0x05060708u, 0x090a0b0cu, 0x0d0e0f10u}, buf + w);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned int old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == (unsigned int)seq * gridDim.x) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
 #ifndef RELAXED
@@ -131,6 +147,30 @@ int main(int argc, char** argv)
         (void)hipStreamSynchronize(s);
         ta.push_back(us_since(t0));
     }
+    // (c) launch per job, completion flag polled by the host
+    unsigned int* counter2 = nullptr;
+    (void)hipMalloc((void**)&counter2, 4);
+    (void)hipMemset(counter2, 0, 4);
+    (void)hipDeviceSynchronize();
+    std::vector<double> tc;
+    uint64_t* dflag = &dmb->pad2[0];
+    uint64_t* hflag = &mb->pad2[0];
+    for (int i = 0; i < 400; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        const uint64_t seq = (uint64_t)i + 1;
+        hipLaunchKernelGGL(xor_flag, dim3(grid), dim3(256), 0, s, dbuf, words, counter2, dflag, seq);
+        bool ok = false;
+        while (us_since(t0) < 1e6) {
+            if (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) == seq) {
+                ok = true;
+                break;
+            }
+        }
+        if (!ok) break;
+        tc.push_back(us_since(t0));
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(counter2);
     // (b) resident service grid
     mb->words = words;
     hipLaunchKernelGGL(service, dim3(grid), dim3(256), 0, ss, dmb, dbuf, counter, 2000000ull /*20 ms*/,
@@ -157,13 +197,14 @@ int main(int argc, char** argv)
     }
     __atomic_store_n(&mb->quit, 1u, __ATOMIC_RELEASE);
     (void)hipStreamSynchronize(ss);
-    // 800 XOR passes with the same pattern (even): the buffer is back to 0x5a
+    // 1200 XOR passes with the same pattern (even): the buffer is back to 0x5a
     bool intact = true;
     const uint8_t* hb = reinterpret_cast<const uint8_t*>(hbuf);
     for (uint32_t i = 0; i < bytes; ++i) intact &= hb[i] == 0x5a;
-    printf("{\"bytes\": %u, \"grid\": %d, \"launch_sync_us\": %.2f, \"service_rtt_us\": %.2f, \"service_jobs\": %zu, "
-           "\"lost\": %d, \"bytes_intact\": %s}\n",
-           bytes, grid, median(ta), tb.empty() ? -1.0 : median(tb), tb.size(), lost, intact ? "true" : "false");
+    printf("{\"bytes\": %u, \"grid\": %d, \"launch_sync_us\": %.2f, \"launch_flag_us\": %.2f, \"flag_jobs\": %zu, "
+           "\"service_rtt_us\": %.2f, \"service_jobs\": %zu, \"lost\": %d, \"bytes_intact\": %s}\n",
+           bytes, grid, median(ta), tc.empty() ? -1.0 : median(tc), tc.size(), tb.empty() ? -1.0 : median(tb),
+           tb.size(), lost, intact ? "true" : "false");
     (void)hipHostFree(hbuf);
     (void)hipHostFree(mb);
     (void)hipFree(counter);
