@@ -338,6 +338,12 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
 void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous);
 void  kmws_arena_free(void* p, int device);
 
+/* Page-locked host memory for the receive / send rings (kmws_rx_batch_attach_ring,
+ * kmws_tx_batch_attach_ring): hipHostMalloc'ed, visible to `device`, so a
+ * caller like kuma needs no HIP headers of its own.  NULL on failure. */
+void* kmws_host_alloc(size_t bytes, int device);
+void  kmws_host_free(void* p);
+
 /* Placement probe for a long-lived batch region inside an arena: times an
  * in-place split-8 unmask of `span` bytes (uniform 64 KiB probe frames, applied
  * twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step, ...

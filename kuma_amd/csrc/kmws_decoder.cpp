@@ -428,6 +428,25 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
     return KMWS_OK;
 }
 
+// ---- pinned host rings ----
+
+void* kmws_host_alloc(size_t bytes, int device)
+{
+    if (bytes == 0 || device < 0 || kmws_device_count() <= device) return nullptr;
+    DevGuard g(device);
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void kmws_host_free(void* p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
 // ---- batched send path (SURVEY f-2) ----
 
 struct kmws_tx_batch {

@@ -39,7 +39,7 @@ EXPORTS = [
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
     "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place",
     "kmws_tx_batch_create", "kmws_tx_batch_destroy", "kmws_tx_batch_add", "kmws_tx_batch_flush",
-    "kmws_tx_batch_pending", "kmws_tx_batch_attach_ring",
+    "kmws_tx_batch_pending", "kmws_tx_batch_attach_ring", "kmws_host_alloc", "kmws_host_free",
 ]
 
 
@@ -123,6 +123,8 @@ def lib() -> C.CDLL:
         "kmws_tx_batch_flush": (C.c_int64, [vp]),
         "kmws_tx_batch_pending": (i32, [vp]),
         "kmws_tx_batch_attach_ring": (i32, [vp, vp, sz]),
+        "kmws_host_alloc": (vp, [sz, i32]),
+        "kmws_host_free": (None, [vp]),
         "kmws_rx_batch_destroy": (None, [vp]),
         "kmws_decoder_feed_deferred": (i32, [vp, vp, u8p, sz, FRAME_CB, vp]),
         "kmws_rx_batch_flush": (i32, [vp]),

@@ -1,0 +1,325 @@
+// BASELINE configs[0] over a real loopback TCP connection: a client thread
+// sends 1,000 x 4 KiB masked TEXT frames to a server thread, which reads the
+// socket in <= 64 KiB reads (kuma's TcpConnection::onReceive,
+// TcpConnection.cpp:220-249) and decodes them (WebSocket::Impl::onWsData ->
+// WSHandler::handleData, WebSocketImpl.cpp:225-246).  Both ends run one codec:
+//   cpu  kuma's codec as restated in oracle/ (byte-loop mask, state machine),
+//        one encode + mask per send, one feed per read -- the reference's shape;
+//   gpu  kmws: sends queued in a kmws_tx_batch over a pinned send ring, one
+//        flush per loop iteration (16 frames), then writev; reads land in a
+//        pinned receive ring fed with kmws_decoder_feed_deferred, one
+//        kmws_rx_batch_flush per loop iteration (socket drained to EAGAIN).
+//        The batches and rings belong to the loop threads (created once); the
+//        decoder is per connection, as kuma's WSHandler.
+// Every delivered payload is compared with what the client sent.  Prints one
+// JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
+//
+// usage: loopback_cfg1 cpu|gpu [reps]
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kmws_gpu.h"
+
+extern "C" {  // oracle/kmws_oracle.c (test infrastructure)
+typedef struct orc_hdr {
+    uint8_t fin, rsv1, rsv2, rsv3, opcode, mask, plen, _pad;
+    uint64_t xpl64;
+    uint8_t maskey[4];
+    uint32_t length;
+} orc_hdr;
+typedef struct orc_decoder orc_decoder;
+typedef int (*orc_frame_cb)(const orc_hdr* hdr, const uint8_t* payload, size_t len, void* user);
+void orc_mask(const uint8_t key[4], uint8_t* data, size_t len, size_t phase);
+int orc_encode_header(const orc_hdr* h, uint8_t out[14]);
+orc_decoder* orc_decoder_create(int mode);
+void orc_decoder_destroy(orc_decoder* d);
+int orc_decoder_feed(orc_decoder* d, uint8_t* data, size_t len, orc_frame_cb cb, void* user);
+}
+
+namespace {
+
+constexpr int kFrames = 1000;
+constexpr size_t kLen = 4096;
+int kGroup = 16;                      // frames per client loop iteration (64 KiB; argv[3])
+size_t kFlushBytes = 0;               // server: hold a drained batch until this many bytes (argv[4]; 0 = every iteration)
+constexpr size_t kRead = 64 * 1024;   // kuma's receive buffer (TcpConnection.cpp:229)
+constexpr size_t kRing = 8u << 20;    // pinned receive ring
+
+uint64_t splitmix(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct Times {  // seconds spent per step in the last connection (breakdown)
+    double tx_flush = 0, writev = 0, rx_feed = 0, rx_flush = 0, recv = 0, client = 0;
+} g_t;
+
+struct Expect {
+    std::vector<uint8_t> plain;  // kFrames * kLen
+    std::atomic<int> got{0};
+    std::atomic<int> bad{0};
+};
+
+void check_frame(Expect* e, const uint8_t* p, size_t len, int opcode)
+{
+    const int k = e->got.load(std::memory_order_relaxed);
+    if (k >= kFrames || len != kLen || opcode != 1 || std::memcmp(p, e->plain.data() + (size_t)k * kLen, kLen) != 0)
+        e->bad.fetch_add(1);
+    e->got.store(k + 1, std::memory_order_release);
+}
+
+int kmws_cb(const kmws_frame_hdr* h, uint8_t* p, size_t len, void* user)
+{
+    check_frame(static_cast<Expect*>(user), p, len, h->opcode);
+    return 0;
+}
+
+int orc_cb(const orc_hdr* h, const uint8_t* p, size_t len, void* user)
+{
+    check_frame(static_cast<Expect*>(user), p, len, h->opcode);
+    return 0;
+}
+
+void send_all(int fd, std::vector<iovec>& iov)
+{
+    size_t i = 0;
+    while (i < iov.size()) {
+        const int cnt = (int)std::min<size_t>(iov.size() - i, 1024);
+        ssize_t w = writev(fd, iov.data() + i, cnt);
+        if (w < 0) {
+            std::perror("writev");
+            std::exit(2);
+        }
+        while (w > 0 && i < iov.size()) {  // advance over what was written
+            if ((size_t)w >= iov[i].iov_len) {
+                w -= (ssize_t)iov[i].iov_len;
+                ++i;
+            } else {
+                iov[i].iov_base = static_cast<uint8_t*>(iov[i].iov_base) + w;
+                iov[i].iov_len -= (size_t)w;
+                w = 0;
+            }
+        }
+    }
+}
+
+// Per loop thread, long-lived (created once, as a loop's batches and rings would be).
+struct LoopObjs {
+    kmws_rx_batch* rx = nullptr;
+    uint8_t* rring = nullptr;
+    kmws_tx_batch* tx = nullptr;
+    uint8_t* sring = nullptr;
+};
+
+// One connection: returns seconds from the first send to the last delivered frame.
+double run_once(bool gpu, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
+{
+    int ls = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = 0;
+    socklen_t al = sizeof a;
+    if (bind(ls, (sockaddr*)&a, sizeof a) != 0 || listen(ls, 1) != 0 || getsockname(ls, (sockaddr*)&a, &al) != 0) {
+        std::perror("listen");
+        std::exit(2);
+    }
+    e.got = 0;
+    e.bad = 0;
+    g_t = Times();
+    std::atomic<bool> ready{false};
+    std::chrono::steady_clock::time_point t_end;
+
+    std::thread server([&] {
+        int fd = accept(ls, nullptr, nullptr);
+        int one = 1;
+        setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        ready = true;
+        if (gpu) {
+            kmws_decoder* d = kmws_decoder_create(KMWS_MODE_SERVER, 0);  // per connection, as in kuma
+            kmws_rx_batch* b = lo.rx;
+            uint8_t* ring = lo.rring;
+            if (!d) std::exit(3);
+            size_t pos = 0;
+            bool closed = false;
+            while (!closed && e.got.load(std::memory_order_acquire) < kFrames) {
+                // one loop iteration: read until the socket is drained, then one GPU batch
+                int flags = 0;
+                for (;;) {
+                    if (pos + kRead > kRing) break;  // ring full: flush first
+                    double t = now_s();
+                    const ssize_t r = recv(fd, ring + pos, kRead, flags);
+                    g_t.recv += now_s() - t;
+                    if (r == 0) closed = true;
+                    if (r <= 0) break;
+                    t = now_s();
+                    if (kmws_decoder_feed_deferred(d, b, ring + pos, (size_t)r, kmws_cb, &e) < 0) std::exit(4);
+                    g_t.rx_feed += now_s() - t;
+                    pos += (size_t)r;
+                    flags = MSG_DONTWAIT;
+                }
+                // throughput policy (argv[4]): keep collecting across iterations until enough
+                // bytes are pending, the ring is full, or every frame has been parsed
+                if (!closed && pos < kFlushBytes && pos + kRead <= kRing &&
+                    e.got.load() + kmws_rx_batch_pending(b) < kFrames)
+                    continue;
+                const double tf = now_s();
+                if (kmws_rx_batch_flush(b) < 0) std::exit(5);
+                g_t.rx_flush += now_s() - tf;
+                pos = 0;  // ring bytes are free again after the flush
+            }
+            kmws_decoder_destroy(d);
+        } else {
+            orc_decoder* d = orc_decoder_create(1);
+            std::vector<uint8_t> buf(kRead);
+            while (e.got.load(std::memory_order_acquire) < kFrames) {
+                const ssize_t r = recv(fd, buf.data(), kRead, 0);
+                if (r <= 0) break;
+                orc_decoder_feed(d, buf.data(), (size_t)r, orc_cb, &e);
+            }
+            orc_decoder_destroy(d);
+        }
+        t_end = std::chrono::steady_clock::now();
+        close(fd);
+    });
+
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (connect(fd, (sockaddr*)&a, sizeof a) != 0) {
+        std::perror("connect");
+        std::exit(2);
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    while (!ready) std::this_thread::yield();
+
+    kmws_tx_batch* tx = lo.tx;
+    uint8_t* sring = lo.sring;
+    std::vector<uint8_t> sbuf;
+    if (!gpu) sbuf.resize(kGroup * kLen);
+    std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hdrs(kGroup);
+    std::vector<int> hlen(kGroup);
+    std::vector<iovec> iov;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int g0 = 0; g0 < kFrames; g0 += kGroup) {
+        const int ng = std::min(kGroup, kFrames - g0);
+        uint8_t* base = gpu ? sring : sbuf.data();
+        // the application writes its payloads (the send buffer is reused per iteration)
+        std::memcpy(base, e.plain.data() + (size_t)g0 * kLen, (size_t)ng * kLen);
+        for (int j = 0; j < ng; ++j) {
+            uint8_t* p = base + (size_t)j * kLen;
+            const uint32_t key = keys[g0 + j];
+            if (gpu) {
+                kmws_frame_hdr h;
+                std::memset(&h, 0, sizeof h);
+                h.fin = 1;
+                h.opcode = KMWS_OP_TEXT;
+                h.mask = 1;
+                std::memcpy(h.maskey, &key, 4);
+                size_t len = kLen;
+                hlen[j] = kmws_tx_batch_add(tx, &h, &p, &len, 1, hdrs[j].data());
+            } else {  // sendWsFrame: mask in place, then encodeFrameHeader (WebSocketImpl.cpp:405-417)
+                orc_hdr h;
+                std::memset(&h, 0, sizeof h);
+                h.fin = 1;
+                h.opcode = 1;
+                h.mask = 1;
+                std::memcpy(h.maskey, &key, 4);
+                orc_mask(h.maskey, p, kLen, 0);
+                h.length = (uint32_t)kLen;
+                hlen[j] = orc_encode_header(&h, hdrs[j].data());
+            }
+        }
+        double tt = now_s();
+        if (gpu && kmws_tx_batch_flush(tx) != ng) std::exit(7);
+        g_t.tx_flush += now_s() - tt;
+        iov.clear();
+        for (int j = 0; j < ng; ++j) {
+            iov.push_back(iovec{hdrs[j].data(), (size_t)hlen[j]});
+            iov.push_back(iovec{base + (size_t)j * kLen, kLen});
+        }
+        tt = now_s();
+        send_all(fd, iov);
+        g_t.writev += now_s() - tt;
+    }
+    g_t.client = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    server.join();
+    close(fd);
+    close(ls);
+    return std::chrono::duration<double>(t_end - t0).count();
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    const std::string mode = argc > 1 ? argv[1] : "cpu";
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
+    if (argc > 3) kGroup = std::max(1, std::atoi(argv[3]));
+    if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
+    const bool gpu = mode == "gpu";
+    if (gpu && kmws_device_count() < 1) {
+        std::printf("{\"mode\": \"gpu\", \"error\": \"no gfx950 device\"}\n");
+        return 1;
+    }
+    Expect e;
+    e.plain.resize((size_t)kFrames * kLen);
+    for (size_t i = 0; i < e.plain.size(); ++i) e.plain[i] = (uint8_t)(0x20 + splitmix(i) % 95);
+    std::vector<uint32_t> keys(kFrames);
+    for (int i = 0; i < kFrames; ++i) keys[i] = (uint32_t)splitmix(0x6b756d61ull + i);
+    LoopObjs lo;
+    if (gpu) {
+        lo.rx = kmws_rx_batch_create(0);
+        lo.rring = static_cast<uint8_t*>(kmws_host_alloc(kRing, 0));
+        lo.tx = kmws_tx_batch_create(0);
+        lo.sring = static_cast<uint8_t*>(kmws_host_alloc((size_t)kGroup * kLen, 0));
+        if (!lo.rx || !lo.rring || !lo.tx || !lo.sring || kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK ||
+            kmws_tx_batch_attach_ring(lo.tx, lo.sring, (size_t)kGroup * kLen) != KMWS_OK)
+            return 3;
+    }
+    double best = 1e9;
+    bool ok = true;
+    for (int r = 0; r < reps + 1; ++r) {  // first connection warms up (staging growth, GPU context)
+        const double t = run_once(gpu, e, keys, lo);
+        ok = ok && e.got.load() == kFrames && e.bad.load() == 0;
+        if (r) best = std::min(best, t);
+    }
+    if (gpu) {
+        kmws_rx_batch_destroy(lo.rx);
+        kmws_tx_batch_destroy(lo.tx);
+        kmws_host_free(lo.rring);
+        kmws_host_free(lo.sring);
+    }
+    const double bytes = (double)kFrames * kLen;
+    std::printf("{\"mode\": \"%s\", \"frames\": %d, \"frame_len\": %zu, \"frames_per_send_iteration\": %d, "
+                "\"rx_flush_bytes\": %zu, \"best_of\": %d, \"GiB_s\": %.3f, \"us_per_frame\": %.3f, "
+                "\"verified\": %s, \"breakdown_ms_last_connection\": {\"client_total\": %.3f, "
+                "\"tx_flush\": %.3f, \"writev\": %.3f, \"server_recv\": %.3f, \"rx_feed\": %.3f, "
+                "\"rx_flush\": %.3f}}\n",
+                mode.c_str(), kFrames, kLen, kGroup, kFlushBytes, reps, bytes / best / (1u << 30),
+                best / kFrames * 1e6, ok ? "true" : "false", g_t.client * 1e3, g_t.tx_flush * 1e3, g_t.writev * 1e3,
+                g_t.recv * 1e3, g_t.rx_feed * 1e3, g_t.rx_flush * 1e3);
+    return ok ? 0 : 1;
+}

@@ -77,3 +77,37 @@ def test_wshandler_adapter_on_gpu(tmp_path):
     exe = _build_adapter(tmp_path)
     r = subprocess.run([str(exe), "gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+def _build_loopback(tmp_path):
+    """tests/cpp/loopback_cfg1.cpp: BASELINE configs[0] over a loopback TCP socket,
+    kmws (GPU) or kuma's codec restated in oracle/ (CPU) on both ends."""
+    lib = kb.build()
+    from oracle import oracle as orc
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    exe = tmp_path / "loopback_cfg1"
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "loopback_cfg1.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", str(exe)])
+    return exe
+
+
+def test_loopback_cfg1_cpu_codec(tmp_path):
+    import json
+    r = subprocess.run([str(_build_loopback(tmp_path)), "cpu", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["verified"] and d["frames"] == 1000
+
+
+@pytest.mark.gpu
+def test_loopback_cfg1_gpu_codec(tmp_path):
+    """1,000 masked frames client -> server over loopback through kmws_tx_batch and
+    the deferred receive batch on a pinned ring: every payload delivered intact."""
+    import json
+    r = subprocess.run([str(_build_loopback(tmp_path)), "gpu", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["verified"] and d["frames"] == 1000
