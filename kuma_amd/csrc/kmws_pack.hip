@@ -577,8 +577,11 @@ __device__ __forceinline__ void edge_block(uint64_t blk, const uint8_t* __restri
 #endif
 // Unit records and edge words in one grid (they are independent, and the
 // record blocks alone are too few to fill the chip): virtual block v < rec_blocks
-// writes records, v >= rec_blocks composes edge words (edge block v - rec_blocks);
-// v = vbase + blockIdx.x, the grid being cut at 2^31 work-items per launch.
+// writes records (record block rec_lo + v), v >= rec_blocks composes edge words
+// (edge block edge_lo + v - rec_blocks); v = vbase + blockIdx.x, the grid being
+// cut at 2^31 work-items per launch.  A frame chunk of the pack pipeline passes
+// the record and edge blocks covering its frames (neighbours' duplicates write
+// identical values).
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock, KMWS_REC_EDGE_WAVES) rec_edge_kernel(const uint8_t* __restrict__ src,
                                                           const uint64_t* __restrict__ start,
@@ -587,14 +590,15 @@ __global__ void __launch_bounds__(kBlock, KMWS_REC_EDGE_WAVES) rec_edge_kernel(c
                                                           const uint16_t* __restrict__ flags, uint32_t n,
                                                           uint64_t cap, UnitRec* __restrict__ rec,
                                                           u32x4* __restrict__ edge, WsHead* __restrict__ head,
-                                                          uint64_t rec_blocks, uint64_t vbase)
+                                                          uint64_t rec_lo, uint64_t rec_blocks, uint64_t edge_lo,
+                                                          uint64_t vbase)
 {
     __shared__ uint32_t s_ub[kBlock + 1];
     const uint64_t v = vbase + blockIdx.x;
     if (v < rec_blocks)
-        unit_rec_block<HEADERS>((uint32_t)v, s_ub, start, ubase, d, flags, n, cap, rec, head);
+        unit_rec_block<HEADERS>((uint32_t)(rec_lo + v), s_ub, start, ubase, d, flags, n, cap, rec, head);
     else
-        edge_block<HEADERS>(v - rec_blocks, src, start, d, flags, n, cap, edge, head);
+        edge_block<HEADERS>(edge_lo + (v - rec_blocks), src, start, d, flags, n, cap, edge, head);
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
@@ -744,7 +748,8 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
                                                       const UnitRec* __restrict__ rec,
                                                       const u32x4* __restrict__ edge,
                                                       const WsHead* __restrict__ head, uint64_t unit_base,
-                                                      uint32_t split)
+                                                      uint32_t split, const uint64_t* __restrict__ chunk_lo,
+                                                      const uint64_t* __restrict__ chunk_hi, uint64_t stride)
 {
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: provably uniform, so the record is one scalar load
@@ -760,24 +765,43 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
         const uint32_t q = gridDim.x / split;
         if (b < q * split) b = (b % split) * q + b / split;
     }
-    const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
-    // record, slot count, status and total are independent scalar loads (one
-    // latency level); slots past the count lie inside the workspace and are ignored
-    const UnitRec r = rec[u];
-    const uint64_t total_units = ubase[n];
+    if (chunk_lo == nullptr) {  // the whole batch in one grid (the default)
+        const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
+        // record, slot count, status and total are independent scalar loads (one
+        // latency level); slots past the count lie inside the workspace and are ignored
+        const UnitRec r = rec[u];
+        const uint64_t total_units = ubase[n];
+        const uint32_t st = head->status;
+        const uint64_t total = start[n];
+        // no early exit between these loads and their uses (the compiler would sink
+        // the record load below the count's wait): an out-of-range wave owns no words
+        const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
+        // keep every field's load above the exit (one wait for all of them)
+        asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
+        if (x.khi == 0) return;  // wave-uniform, after the record's wait
+        // Every load is issued before the first store (vmcnt also counts stores, so
+        // a load issued after a store would make its wait cover that store too).
+        UnitRegs R;
+        unit_issue(x, lane, src, edge, R);
+        unit_finish(x, lane, dst, total, R);
+        return;
+    }
+    // One chunk of the pack pipeline: units [*chunk_lo, *chunk_hi) (the unit
+    // bases of the chunk's first frame and of the next chunk's), grid-strided
+    // by `stride` units since the host cannot size the grid to the chunk.
+    const uint64_t u_lo = *chunk_lo, u_hi = *chunk_hi;
     const uint32_t st = head->status;
     const uint64_t total = start[n];
-    // no early exit between these loads and their uses (the compiler would sink
-    // the record load below the count's wait): an out-of-range wave owns no words
-    const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
-    // keep every field's load above the exit (one wait for all of them)
-    asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
-    if (x.khi == 0) return;  // wave-uniform, after the record's wait
-    // Every load is issued before the first store (vmcnt also counts stores, so
-    // a load issued after a store would make its wait cover that store too).
-    UnitRegs R;
-    unit_issue(x, lane, src, edge, R);
-    unit_finish(x, lane, dst, total, R);
+    for (uint64_t u = u_lo + unit_base + (uint64_t)b * (kBlock / 64) + wave; u < u_hi; u += stride) {
+        const UnitRec r = rec[u];
+        const UnitInfo x = decode_unit(r, st == 0, src);
+        asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
+        if (x.khi != 0) {
+            UnitRegs R;
+            unit_issue(x, lane, src, edge, R);
+            unit_finish(x, lane, dst, total, R);
+        }
+    }
 }
 
 // ------------------------------ header unpack / validate ------------------------------
@@ -952,6 +976,43 @@ static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, 
     return hip_status(hipGetLastError());
 }
 
+// Side stream + events of the pack pipeline, one set per (host thread, device):
+// kmws calls come from each event loop's own thread, on that loop's stream.
+constexpr uint32_t kMaxPackChunks = 8;
+constexpr int kPackDevices = 16;
+struct PackSide {
+    hipStream_t ss;
+    hipEvent_t fork, ev[kMaxPackChunks];
+    bool ready;
+};
+static PackSide* pack_side()
+{
+    thread_local PackSide side[kPackDevices];  // created on first use, kept for the thread's life
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kPackDevices) return nullptr;
+    PackSide& p = side[dev];
+    if (!p.ready) {
+        if (hipStreamCreateWithFlags(&p.ss, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&p.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+        for (uint32_t j = 0; j < kMaxPackChunks; ++j)
+            if (hipEventCreateWithFlags(&p.ev[j], hipEventDisableTiming) != hipSuccess) return nullptr;
+        p.ready = true;
+    }
+    return &p;
+}
+
+// Frame chunks of the pack pipeline (1 = one record/edge grid, then one copy
+// grid).  KMWS_PACK_CHUNKS overrides it (tuning).
+static uint32_t pack_chunks(uint32_t n)
+{
+    static const uint32_t k = [] {
+        const char* e = getenv("KMWS_PACK_CHUNKS");
+        const int v = e ? atoi(e) : 1;
+        return v < 1 ? 1u : (v > (int)kMaxPackChunks ? kMaxPackChunks : (uint32_t)v);
+    }();
+    return (uint64_t)n >= (uint64_t)k * kBlock ? k : 1u;  // at least one record block per chunk
+}
+
 template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, const uint64_t* start,
                                const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
@@ -959,10 +1020,6 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     const uint32_t fb = (n + kBlock - 1) / kBlock;
     const uint64_t eb = ((uint64_t)n + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
     constexpr uint64_t kMaxBlocks = (1ull << 31) / kBlock;  // stay below 2^31 work-items per launch
-    for (uint64_t v0 = 0, nv = fb + eb; v0 < nv; v0 += kMaxBlocks)
-        hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
-                           dim3(kBlock), 0, s, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
-                           (uint64_t)fb, v0);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
     // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
     // batches of small frames need every wave slot to hide their per-unit
@@ -983,11 +1040,47 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
     constexpr uint64_t kWavesPerBlock = kBlock / 64;
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
-    for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
-        const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
-        hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0,
-                           split);
+    const uint32_t K = pack_chunks(n);
+    if (K == 1) {
+        for (uint64_t v0 = 0, nv = fb + eb; v0 < nv; v0 += kMaxBlocks)
+            hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
+                               dim3(kBlock), 0, s, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
+                               (uint64_t)0, (uint64_t)fb, (uint64_t)0, v0);
+        for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
+            const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
+            hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
+                               dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head,
+                               u0, split, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)0);
+        }
+        return hip_status(hipGetLastError());
+    }
+    // Pipeline: the record/edge grids of the K frame chunks run back to back on a
+    // side stream while the copy grid of chunk j (caller's stream) waits only for
+    // chunk j's records, so all but the first chunk's prologue hides under copies.
+    // Fork and join are events, so the call stays stream-ordered and capturable.
+    PackSide* ps = pack_side();
+    if (!ps) return KMWS_ERR_FAILED;
+    if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->ss, ps->fork, 0) != hipSuccess)
+        return KMWS_ERR_FAILED;
+    for (uint32_t j = 0; j < K; ++j) {
+        const uint64_t F0 = (uint64_t)n * j / K, F1 = (uint64_t)n * (j + 1) / K;
+        const uint64_t r0 = F0 / kBlock, r1 = (F1 + kBlock - 1) / kBlock;
+        const uint64_t e0 = F0 / kEdgeFramesPerBlock, e1 = (F1 + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
+        for (uint64_t v0 = 0, nv = (r1 - r0) + (e1 - e0); v0 < nv; v0 += kMaxBlocks)
+            hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
+                               dim3(kBlock), 0, ps->ss, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
+                               r0, r1 - r0, e0, v0);
+        if (hipEventRecord(ps->ev[j], ps->ss) != hipSuccess) return KMWS_ERR_FAILED;
+    }
+    uint64_t gw = (units + K - 1) / K;  // waves per chunk grid (equal chunks: one unit each)
+    gw = (gw + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    gw = gw < kMaxUnitsPerLaunch ? gw : kMaxUnitsPerLaunch;
+    for (uint32_t j = 0; j < K; ++j) {
+        const uint64_t F0 = (uint64_t)n * j / K, F1 = (uint64_t)n * (j + 1) / K;
+        if (hipStreamWaitEvent(s, ps->ev[j], 0) != hipSuccess) return KMWS_ERR_FAILED;
+        hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)(gw / kWavesPerBlock)), dim3(kBlock), lds_pad, s, src,
+                           dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, (uint64_t)0, split,
+                           (const uint64_t*)(c.ubase + F0), (const uint64_t*)(c.ubase + F1), gw);
     }
     return hip_status(hipGetLastError());
 }
