@@ -225,3 +225,16 @@ def test_unpack_quirk127_lengths(T):
         T.cuda.synchronize()
         assert int(out_err.cpu()[0]) == err, ext
         assert int(out_desc.cpu().numpy()[0, 1] & 0xFFFFFFFF) == L
+
+
+@pytest.mark.parametrize("chunks", [3, 8])
+def test_pack_chunks_knob(T, chunks):
+    """The chunked pack pipeline (KMWS_PACK_CHUNKS, read once per process) in a
+    child process: encode and gather-unmask bit-exact vs the oracle."""
+    import subprocess
+    import sys
+    env = dict(os.environ, KMWS_PACK_CHUNKS=str(chunks))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "pack_chunks_child.py")], env=env,
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert f"pack chunks ok {chunks}" in r.stdout
