@@ -322,7 +322,11 @@ kmws_status kmws_pipeline_set_transfer(kmws_pipeline* p, int mode);
 /* In-place unmask of frames that live in HOST memory (descs on the host,
  * offsets relative to host_base, sorted, within span).  Synchronous: returns
  * when every byte is back in host_base.  Only the frames' extents are written
- * back by the copy path; the zero-copy path rewrites their 16-B hulls. */
+ * back by the copy path; the zero-copy path rewrites their 16-B hulls.
+ * Every descriptor is checked before anything is queued: unsorted, overlapping
+ * or out-of-span frames return KMWS_ERR_INVALID_PARAM, a frame whose 16-B hull
+ * exceeds chunk_bytes KMWS_ERR_BUFFER_TOO_SMALL, with host_base untouched; a
+ * HIP failure mid-batch drains every queued copy before returning. */
 kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t span, const kmws_desc* descs,
                                  uint32_t n);
 

@@ -580,8 +580,7 @@ __device__ __forceinline__ void edge_block(uint64_t blk, const uint8_t* __restri
 // writes records (record block rec_lo + v), v >= rec_blocks composes edge words
 // (edge block edge_lo + v - rec_blocks); v = vbase + blockIdx.x, the grid being
 // cut at 2^31 work-items per launch.  A frame chunk of the pack pipeline passes
-// the record and edge blocks covering its frames (neighbours' duplicates write
-// identical values).
+// the record and edge blocks it owns (launch_copy: each block in one chunk).
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock, KMWS_REC_EDGE_WAVES) rec_edge_kernel(const uint8_t* __restrict__ src,
                                                           const uint64_t* __restrict__ start,
@@ -749,7 +748,8 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
                                                       const u32x4* __restrict__ edge,
                                                       const WsHead* __restrict__ head, uint64_t unit_base,
                                                       uint32_t split, const uint64_t* __restrict__ chunk_lo,
-                                                      const uint64_t* __restrict__ chunk_hi, uint64_t stride)
+                                                      const uint64_t* __restrict__ chunk_hi, uint64_t stride,
+                                                      uint64_t slots)
 {
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: provably uniform, so the record is one scalar load
@@ -788,13 +788,17 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     }
     // One chunk of the pack pipeline: units [*chunk_lo, *chunk_hi) (the unit
     // bases of the chunk's first frame and of the next chunk's), grid-strided
-    // by `stride` units since the host cannot size the grid to the chunk.
-    const uint64_t u_lo = *chunk_lo, u_hi = *chunk_hi;
+    // by `stride` units since the host cannot size the grid to the chunk.  A
+    // batch whose records were not written (status set: the wire exceeds
+    // dst_cap, so the unit bases may run past the `slots` records the
+    // workspace holds) reads no record at all; u_hi is clamped to `slots` too.
     const uint32_t st = head->status;
+    if (st != 0) return;
+    const uint64_t u_lo = *chunk_lo, u_hi = *chunk_hi < slots ? *chunk_hi : slots;
     const uint64_t total = start[n];
     for (uint64_t u = u_lo + unit_base + (uint64_t)b * (kBlock / 64) + wave; u < u_hi; u += stride) {
         const UnitRec r = rec[u];
-        const UnitInfo x = decode_unit(r, st == 0, src);
+        const UnitInfo x = decode_unit(r, true, src);
         asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
         if (x.khi != 0) {
             UnitRegs R;
@@ -1050,7 +1054,7 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
             const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
             hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
                                dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head,
-                               u0, split, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)0);
+                               u0, split, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)0, units);
         }
         return hip_status(hipGetLastError());
     }
@@ -1058,14 +1062,25 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     // side stream while the copy grid of chunk j (caller's stream) waits only for
     // chunk j's records, so all but the first chunk's prologue hides under copies.
     // Fork and join are events, so the call stays stream-ordered and capturable.
+    // Chunk boundaries are whole record blocks (F_j = 256 R_j), and each edge
+    // block belongs to the chunk holding its first frame (blocks
+    // [ceil(F_j / 51), ceil(F_j+1 / 51))): every record and edge block is
+    // written exactly once, and chunk j's copy (which waits for the grids of
+    // chunks 0..j, issued in order on one stream) needs no block of a later
+    // chunk -- no grid writes what a running copy grid reads.
     PackSide* ps = pack_side();
     if (!ps) return KMWS_ERR_FAILED;
     if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->ss, ps->fork, 0) != hipSuccess)
         return KMWS_ERR_FAILED;
+    auto chunk_frame = [&](uint32_t j) -> uint64_t {  // first frame of chunk j (j = K: n)
+        const uint64_t f = (uint64_t)kBlock * ((uint64_t)fb * j / K);
+        return f < n ? f : n;
+    };
+    auto edge_blk = [](uint64_t f) { return (f + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock; };
     for (uint32_t j = 0; j < K; ++j) {
-        const uint64_t F0 = (uint64_t)n * j / K, F1 = (uint64_t)n * (j + 1) / K;
+        const uint64_t F0 = chunk_frame(j), F1 = chunk_frame(j + 1);
         const uint64_t r0 = F0 / kBlock, r1 = (F1 + kBlock - 1) / kBlock;
-        const uint64_t e0 = F0 / kEdgeFramesPerBlock, e1 = (F1 + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
+        const uint64_t e0 = edge_blk(F0), e1 = edge_blk(F1);
         for (uint64_t v0 = 0, nv = (r1 - r0) + (e1 - e0); v0 < nv; v0 += kMaxBlocks)
             hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
                                dim3(kBlock), 0, ps->ss, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
@@ -1076,11 +1091,11 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     gw = (gw + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
     gw = gw < kMaxUnitsPerLaunch ? gw : kMaxUnitsPerLaunch;
     for (uint32_t j = 0; j < K; ++j) {
-        const uint64_t F0 = (uint64_t)n * j / K, F1 = (uint64_t)n * (j + 1) / K;
+        const uint64_t F0 = chunk_frame(j), F1 = chunk_frame(j + 1);
         if (hipStreamWaitEvent(s, ps->ev[j], 0) != hipSuccess) return KMWS_ERR_FAILED;
         hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)(gw / kWavesPerBlock)), dim3(kBlock), lds_pad, s, src,
                            dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, (uint64_t)0, split,
-                           (const uint64_t*)(c.ubase + F0), (const uint64_t*)(c.ubase + F1), gw);
+                           (const uint64_t*)(c.ubase + F0), (const uint64_t*)(c.ubase + F1), gw, units);
     }
     return hip_status(hipGetLastError());
 }

@@ -157,27 +157,38 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
             return KMWS_ERR_FAILED;
         return status == 0 ? KMWS_OK : KMWS_ERR_INVALID_PARAM;
     }
+    // Every descriptor is checked before the first chunk is queued (sorted, in
+    // the span, each frame's 16-B aligned hull within one chunk), so a bad batch
+    // is rejected with nothing in flight and the host buffer untouched.
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t off = descs[i].off, end = off + descs[i].len;
+        if (end < off || end > span || (i && off < descs[i - 1].off + descs[i - 1].len))
+            return KMWS_ERR_INVALID_PARAM;
+        if (end - (off & ~(uint64_t)15) > p->chunk) return KMWS_ERR_BUFFER_TOO_SMALL;  // one frame larger than a chunk
+    }
     uint32_t f = 0;
     size_t k = 0;
     kmws_status st = KMWS_OK;
+    // From here on every failure leaves the loop and goes through the drain
+    // below: no slot is still copying into host_base when the call returns.
     while (f < n && st == KMWS_OK) {
-        // frames [f, e) whose 16-B aligned hull fits the chunk
+        // frames [f, e) whose 16-B aligned hull fits the chunk (e > f: checked above)
         const uint64_t lo = descs[f].off & ~(uint64_t)15;
-        if (descs[f].off + descs[f].len > span) return KMWS_ERR_INVALID_PARAM;
         uint32_t e = f;
         uint64_t hi = descs[f].off;
         while (e < n && e - f < p->max_frames) {
             const uint64_t end = descs[e].off + descs[e].len;
-            if (descs[e].off < hi || end > span) return KMWS_ERR_INVALID_PARAM;  // sorted, in range
             if (end - lo > p->chunk) break;
             hi = end;
             ++e;
         }
-        if (e == f) return KMWS_ERR_BUFFER_TOO_SMALL;  // one frame larger than a chunk
         // at most 3 slots in flight: with 4, H2D runs far enough ahead to hold
         // the DMA engines the D2H needs (26 GiB/s instead of 45)
         kmws_pipeline::Slot& s = p->slots[k % std::min<size_t>(p->slots.size(), 3)];
-        if (s.busy && hipEventSynchronize(s.done) != hipSuccess) return KMWS_ERR_FAILED;
+        if (s.busy && hipEventSynchronize(s.done) != hipSuccess) {
+            st = KMWS_ERR_FAILED;
+            break;
+        }
         s.busy = false;
         const uint64_t first = descs[f].off;
         for (uint32_t i = f; i < e; ++i) {
@@ -190,8 +201,17 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
             hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)(e - f) * sizeof(kmws_desc), hipMemcpyHostToDevice,
                            p->s_in) != hipSuccess ||
             hipEventRecord(s.in_done, p->s_in) != hipSuccess ||
-            hipStreamWaitEvent(p->s_kern, s.in_done, 0) != hipSuccess)
-            return KMWS_ERR_FAILED;
+            hipStreamWaitEvent(p->s_kern, s.in_done, 0) != hipSuccess) {
+            st = KMWS_ERR_FAILED;
+            break;
+        }
+        // the H2D copies may be in flight: the slot counts as busy until its
+        // last recorded event (s_in's work is drained below in any case)
+        s.busy = true;
+        if (hipEventRecord(s.done, p->s_in) != hipSuccess) {
+            st = KMWS_ERR_FAILED;
+            break;
+        }
         st = kmws_unmask_batch(s.d_buf, bytes, s.d_desc, e - f, s.d_ws, s.ws_bytes, p->s_kern);
         if (st != KMWS_OK) break;
         // write back exactly the frames' extent: neighbours' bytes stay untouched
@@ -199,11 +219,15 @@ kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t 
             hipStreamWaitEvent(p->s_out, s.kern_done, 0) != hipSuccess ||
             hipMemcpyAsync(host_base + first, s.d_buf + (first - lo), hi - first, hipMemcpyDeviceToHost,
                            p->s_out) != hipSuccess ||
-            hipEventRecord(s.done, p->s_out) != hipSuccess)
-            return KMWS_ERR_FAILED;
-        s.busy = true;
+            hipEventRecord(s.done, p->s_out) != hipSuccess) {
+            st = KMWS_ERR_FAILED;
+            break;
+        }
         f = e;
         ++k;
+    }
+    if (st != KMWS_OK) {  // whatever was queued finishes before the caller gets its buffer back
+        for (hipStream_t q : {p->s_in, p->s_kern, p->s_out}) (void)hipStreamSynchronize(q);
     }
     for (auto& s : p->slots) {
         if (s.busy && hipEventSynchronize(s.done) != hipSuccess) st = KMWS_ERR_FAILED;

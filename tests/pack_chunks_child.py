@@ -46,6 +46,29 @@ def main():
             assert ws.status() == 0, ("gather", kind, aligned)
             orig = b"".join(bytes(src[int(o):int(o) + int(L)]) for o, L in zip(offs, lens))
             assert bytes(dst.cpu().numpy()[:P]) == orig, ("gather", kind, aligned)
+    # dst too small: the wire exceeds dst_cap, so the unit bases run past the
+    # records the workspace holds; the status word is set, nothing is written
+    # and (the point) no copy wave reads a record slot past the workspace
+    n = 16 * 640
+    rng = np.random.default_rng(zlib.crc32(b"chunks-small-dst"))
+    lens, flags, keys = frames(rng, "frag4k", n)
+    src, offs = src_arena(rng, lens, True)
+    want, _ = orc.encode_batch(src, offs, lens, flags, keys)
+    for cap in (len(want) - 1, len(want) // 4):
+        got, off, st, total = gpu_encode(T, src, offs, lens, flags, keys, cap=cap)
+        assert st != 0, ("encode small dst", cap)
+        assert (got == 0xEE).all(), ("encode small dst wrote", cap)
+    descs = kmws.make_descs(offs.astype(np.int64), lens, keys.astype(np.int64))
+    d_src = T.from_numpy(np.concatenate([src, np.zeros((-len(src)) % 16 + 16, np.uint8)])).cuda()
+    P = int(lens.sum())
+    for cap in (P - 1, P // 4):
+        dst = T.full((cap - cap % 16,), 0xEE, dtype=T.uint8, device="cuda")
+        dst_off = T.zeros(n + 1, dtype=T.int64, device="cuda")
+        ws = kmws.Workspace(kmws.copy_workspace_size(n, dst.numel()))
+        kmws.gather_unmask(d_src, descs, dst, dst_off, ws)
+        T.cuda.synchronize()
+        assert ws.status() != 0, ("gather small dst", cap)
+        assert bool((dst == 0xEE).all()), ("gather small dst wrote", cap)
     print("pack chunks ok", os.environ["KMWS_PACK_CHUNKS"])
 
 

@@ -69,3 +69,38 @@ def test_pipeline_rejects_oversized_frame(kmws):
     d["off"][2] = d["off"][1] + 200010
     with pytest.raises(RuntimeError):
         kmws.Pipeline(0, 65536, 16, 2).unmask(buf, d)
+
+
+@pytest.mark.parametrize("defect,code", [("unsorted", -8), ("out_of_span", -8), ("oversized", -17)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_pipeline_late_bad_descriptor_leaves_buffer_untouched(kmws, defect, code, pinned):
+    """A defect in the LAST descriptor (after many chunks' worth of good frames)
+    is reported before any chunk is queued: the call fails with the reference's
+    error value and not one byte of the host buffer has been rewritten."""
+    import torch
+    rng = np.random.default_rng(77 + len(defect))
+    buf, d = wire_like(rng, 400, 60000)
+    if defect == "unsorted":
+        d["off"][-1] = d["off"][-3]
+    elif defect == "out_of_span":
+        d["len"][-1] = buf.nbytes  # runs past the span
+    else:  # a frame larger than one chunk, placed after the others
+        big = np.zeros(buf.nbytes + 300000, np.uint8)
+        big[:buf.nbytes] = buf
+        buf = big
+        d["off"][-1] = d["off"][-2] + d["len"][-2] + 16
+        d["len"][-1] = 200000
+    orig = buf.copy()
+    host = torch.from_numpy(buf).pin_memory() if pinned else buf
+    # COPY transfer: the chunked ring (the path that used to queue earlier chunks)
+    p = kmws.Pipeline(0, 1 << 17, 1 << 16, 3, transfer=1)
+    with pytest.raises(RuntimeError, match=f"kmws_status {code}"):
+        p.unmask(host, d)
+    got = host.numpy() if pinned else host
+    assert np.array_equal(got, orig)
+    # the pipeline stays usable: a good batch afterwards is exact
+    good, gd = wire_like(rng, 300, 60000)
+    want = good.copy()
+    orc.unmask_batch(want, gd)
+    p.unmask(good, gd)
+    assert np.array_equal(good, want)
