@@ -7,10 +7,9 @@
 //   1. scan_reduce / scan_partials / scan_emit: one exclusive scan of two
 //      per-frame values -- the wire size (2/4/10 + 4*mask + len) -> wire_off,
 //      and an upper bound on the frame's wave units -> unit slot bases;
-//   2. rec_edge_kernel, one grid for two independent jobs: one 32-byte record
-//      per wave unit (slots written coalesced), and the few words around each
-//      frame boundary (header bytes, the next frame's first bytes), composed
-//      byte-exactly;
+//   2. prologue_kernel, 256 frames per block: the few words around each
+//      frame's boundaries (header bytes, the next frame's first bytes),
+//      composed byte-exactly, and one 32-byte record per wave unit;
 //   3. copy_kernel: one wave per unit of a frame's owned 64-byte granules;
 //      interior words are loaded, funnel-shifted and XORed with the rotated
 //      key, edge words are merged in; every granule is written once, by one
@@ -372,33 +371,6 @@ struct UnitRec {
 };
 static_assert(sizeof(UnitRec) == 32, "UnitRec is one s_load_dwordx8");
 
-// Adds frame h's bytes (header, then masked payload) that fall in [a, a + 16).
-template <bool HEADERS>
-__device__ __forceinline__ void add_frame(u32x4& out, uint64_t a, const FrameGeom& h, uint32_t fl,
-                                          const uint8_t* __restrict__ src)
-{
-    if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
-        uint64_t h0, h1;
-        build_header(h.len, fl, h.key, h0, h1);
-        const int s = (int)((int64_t)h.r0 - (int64_t)a);
-        const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-        const int he = (int)(h.p0 - h.r0) + s;
-        out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
-    }
-    if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
-        const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
-        const uint64_t slo = lo_b + h.sdel, shi = hi_b + h.sdel;
-        const uint64_t s0 = slo & ~(uint64_t)15, s1 = (shi - 1) & ~(uint64_t)15;
-        const u32x4 W0 = *reinterpret_cast<const u32x4*>(src + s0);
-        const u32x4 W1 = s1 != s0 ? *reinterpret_cast<const u32x4*>(src + s1) : W0;
-        const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
-        const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd)
-                                : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
-        const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
-        out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
-    }
-}
-
 // Geometry (and flags) of frames f, f+1, f+2 -- the frames a word starting in
 // frame f overlaps in all but tiny-frame batches -- loaded at once (indices
 // clamped instead of branches, so the loads issue together).
@@ -430,174 +402,276 @@ __device__ __forceinline__ void load_geoms(uint32_t f, uint32_t n, FrameGeom (&g
     }
 }
 
-// Output word [a, a + 16) composed from every frame from f on that overlaps it
-// (g, fl: load_geoms(f)).  The payload source words of the three frames are
-// loaded together (src + 0 where a frame has none); frames past f+2 are
-// walked one by one.
+// Output word [a, a + 16) composed byte by byte from every frame from f on that
+// overlaps it -- the rare word three or more regions reach into (frames shorter
+// than a word); few registers, one frame's geometry at a time.
 template <bool HEADERS>
-__device__ u32x4 compose_word(uint64_t a, uint32_t f, uint32_t n, const FrameGeom (&g)[kPre],
-                              const uint32_t (&fl)[kPre], const uint8_t* __restrict__ src,
-                              const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
-                              const uint16_t* __restrict__ flags)
+__device__ __attribute__((noinline)) u32x4 compose_word_bytes(uint64_t a, uint32_t f, uint32_t n,
+                                                              const uint8_t* __restrict__ src,
+                                                              const uint64_t* __restrict__ start,
+                                                              const kmws_desc* __restrict__ d,
+                                                              const uint16_t* __restrict__ flags)
 {
-    u32x4 W0[kPre], W1[kPre];
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-        const FrameGeom& h = g[i];
-        const bool pay = h.r0 < a + 16 && h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a;
-        const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
-        const uint64_t s0 = pay ? (lo_b + h.sdel) & ~(uint64_t)15 : 0;
-        const uint64_t s1 = pay ? (hi_b + h.sdel - 1) & ~(uint64_t)15 : 0;
-        W0[i] = *reinterpret_cast<const u32x4*>(src + s0);
-        W1[i] = *reinterpret_cast<const u32x4*>(src + s1);
-    }
     u32x4 out = u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-        const FrameGeom& h = g[i];
-        if (h.r0 >= a + 16) continue;
-        if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
+    uint32_t j = f;
+    FrameGeom h = geom<HEADERS>(j, start, d, flags);
+    uint32_t flj = HEADERS ? flags[j] : 0u;
+    for (uint32_t b = 0; b < 16; ++b) {
+        const uint64_t x = a + b;
+        while (x >= h.r1 && j + 1 < n) {
+            ++j;
+            h = geom<HEADERS>(j, start, d, flags);
+            flj = HEADERS ? flags[j] : 0u;
+        }
+        if (x < h.r0 || x >= h.r1) continue;  // past the last region
+        uint32_t v;
+        if (x < h.p0) {  // header byte x - r0
             uint64_t h0, h1;
-            build_header(h.len, fl[i], h.key, h0, h1);
-            const int s = (int)((int64_t)h.r0 - (int64_t)a);
-            const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-            const int he = (int)(h.p0 - h.r0) + s;
-            out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
+            build_header(h.len, flj, h.key, h0, h1);
+            const uint32_t k = (uint32_t)(x - h.r0);
+            v = (uint32_t)((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8))) & 0xFFu);
+        } else {  // payload byte: data[i] ^ key[i % 4]
+            v = src[x + h.sdel] ^ ((h.key >> (8 * ((x - h.p0) & 3u))) & 0xFFu);
         }
-        if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
-            const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
-            const uint64_t s0 = (lo_b + h.sdel) & ~(uint64_t)15;
-            const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
-            const u32x4 V = dd >= 0 ? funnel16(W0[i], W1[i], (uint32_t)dd)
-                                    : funnel16(u32x4{0, 0, 0, 0}, W0[i], (uint32_t)(16 + dd));
-            const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
-            out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
-        }
-    }
-    if (g[kPre - 1].r0 < a + 16) {
-        for (uint32_t j = f + kPre; j < n; ++j) {
-            const FrameGeom h = geom<HEADERS>(j, start, d, flags);
-            if (h.r0 >= a + 16) break;
-            add_frame<HEADERS>(out, a, h, HEADERS ? flags[j] : 0u, src);
-        }
+        const uint32_t sh = 8u * (b & 3u), q = b >> 2;
+        if (q == 0) out.x |= v << sh;
+        else if (q == 1) out.y |= v << sh;
+        else if (q == 2) out.z |= v << sh;
+        else out.w |= v << sh;
     }
     return out;
 }
 
-// Unit records of 256 frames per block, written slot by slot (coalesced): each
-// slot finds its frame by a binary search over the block's slot bases in LDS.
-// Frame f owns slots [ubase[f], ubase[f+1]); slots past its exact unit count
-// are marked empty.  Also the capacity check (status set if total > cap).
-template <bool HEADERS>
-__device__ __forceinline__ void unit_rec_block(uint32_t blk, uint32_t* s_ub, const uint64_t* __restrict__ start,
-                                               const uint64_t* __restrict__ ubase, const kmws_desc* __restrict__ d,
-                                               const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
-                                               UnitRec* __restrict__ rec, WsHead* __restrict__ head)
+// Payload source words of frame h for the output word [a, a + 16): the aligned
+// words holding its first and last payload byte there (src + 0 when it has none).
+__device__ __forceinline__ void pay_words(bool live, const FrameGeom& h, uint64_t a, const uint8_t* __restrict__ src,
+                                          u32x4& W0, u32x4& W1)
 {
-    const uint32_t f0 = blk * kBlock;
-    const uint64_t total = start[n];
-    if (total > cap) {  // records would not fit the workspace; the copy waves see the status
-        if (blk == 0 && threadIdx.x == 0) atomicOr(&head->status, kStatusBadDesc);
-        return;
+    const bool pay = live && h.r0 < a + 16 && h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a;
+    const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+    const uint64_t s0 = pay ? (lo_b + h.sdel) & ~(uint64_t)15 : 0;
+    const uint64_t s1 = pay ? (hi_b + h.sdel - 1) & ~(uint64_t)15 : 0;
+    W0 = *reinterpret_cast<const u32x4*>(src + s0);
+    W1 = *reinterpret_cast<const u32x4*>(src + s1);
+}
+
+// Frame h's bytes (header, then masked payload) in [a, a + 16), its payload
+// words W0/W1 from pay_words.
+template <bool HEADERS>
+__device__ __forceinline__ void put_frame(u32x4& out, uint64_t a, const FrameGeom& h, uint32_t fl, const u32x4& W0,
+                                          const u32x4& W1)
+{
+    if (h.r0 >= a + 16) return;
+    if (HEADERS && h.p0 > a && h.p0 > h.r0) {  // header bytes [r0, p0)
+        uint64_t h0, h1;
+        build_header(h.len, fl, h.key, h0, h1);
+        const int s = (int)((int64_t)h.r0 - (int64_t)a);
+        const u32x4 H = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+        const int he = (int)(h.p0 - h.r0) + s;
+        out |= shift_in(H, s) & byte_range(s < 0 ? 0 : s, he > 16 ? 16 : he);
     }
-    const uint32_t nf = n - f0 < (uint32_t)kBlock ? n - f0 : (uint32_t)kBlock;
-    const uint64_t S0 = ubase[f0];
-    if (threadIdx.x < nf) s_ub[threadIdx.x] = (uint32_t)(ubase[f0 + threadIdx.x] - S0);
-    if (threadIdx.x == 0) s_ub[nf] = (uint32_t)(ubase[f0 + nf] - S0);  // nf may be kBlock
-    __syncthreads();
-    const uint32_t ns = s_ub[nf];
-    const uint64_t total_words = (total + 15) >> 4;
-    for (uint32_t s = threadIdx.x; s < ns; s += kBlock) {
-        uint32_t lo = 0, hi = nf;  // s_ub[lo] <= s < s_ub[hi]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_ub[mid] <= s) lo = mid; else hi = mid;
-        }
-        const uint32_t f = f0 + lo;
-        const uint64_t m = s - s_ub[lo];
-        const FrameGeom g = geom<HEADERS>(f, start, d, flags);
-        const FrameWords w = frame_words(g, total_words);
-        UnitRec r;
-        if (m < w.units) {
-            const uint64_t b = w.b0 + m * kUnitWords;
-            auto rel = [&](uint64_t x) -> uint32_t {
-                return (uint32_t)(x <= b ? 0 : (x - b >= (uint64_t)kUnitWords ? kUnitWords : x - b));
-            };
-            r.dst = 16u * b;
-            r.src = 16u * b + g.sdel;
-            r.f = f;
-            r.rk = g.key ? rot_key(g.key, g.p0) : 0u;
-            const uint32_t klo = rel(w.olo), khi = rel(w.ohi), ilo = rel(w.ilo), ihi = rel(w.ihi);
-            const uint32_t head_f = (uint32_t)(w.ilo - w.olo);
-            r.own = klo | head_f << 12 | khi << 16;
-            r.inner = ilo | ihi << 16;
-            if (head_f + (khi - ihi) > (uint32_t)kEdgeWords || ilo - klo > head_f)  // cannot happen
-                atomicOr(&head->status, kStatusBadDesc);
-        } else {
-            r.dst = r.src = 0;
-            r.f = r.rk = 0;
-            r.own = r.inner = 0;
-        }
-        rec[S0 + s] = r;
+    if (h.r1 > h.p0 && h.p0 < a + 16 && h.r1 > a) {  // payload bytes
+        const uint64_t lo_b = h.p0 > a ? h.p0 : a, hi_b = h.r1 < a + 16 ? h.r1 : a + 16;
+        const uint64_t s0 = (lo_b + h.sdel) & ~(uint64_t)15;
+        const int dd = (int)((int64_t)(a + h.sdel) - (int64_t)s0);  // in [-15, 15]
+        const u32x4 V = dd >= 0 ? funnel16(W0, W1, (uint32_t)dd) : funnel16(u32x4{0, 0, 0, 0}, W0, (uint32_t)(16 + dd));
+        const uint32_t rk = h.key ? rot_key(h.key, h.p0) : 0u;
+        out |= (V ^ rk) & byte_range((int)(lo_b - a), (int)(hi_b - a));
     }
 }
 
-// A frame's edge words -- its owned words outside its interior: q < head_f at
-// olo + q, then the tail at ihi + (q - head_f) -- composed one thread per
-// (frame, q) into edge[f * kEdgeWords + q].
-constexpr int kEdgeFramesPerBlock = kBlock / kEdgeWords;  // 51 frames, 255 threads
-template <bool HEADERS>
-__device__ __forceinline__ void edge_block(uint64_t blk, const uint8_t* __restrict__ src,
-                                           const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
-                                           const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
-                                           u32x4* __restrict__ edge, const WsHead* __restrict__ head)
-{
-    const uint32_t t = threadIdx.x;
-    const uint64_t f64 = blk * kEdgeFramesPerBlock + t / kEdgeWords;
-    if (t >= (uint32_t)(kEdgeFramesPerBlock * kEdgeWords) || f64 >= n) return;
-    const uint32_t f = (uint32_t)f64, q = t % kEdgeWords;
-    // total, status and the three frames' geometry: one latency level
-    const uint64_t total = start[n];
-    const uint32_t st = head->status;
-    FrameGeom g[kPre];
-    uint32_t fl[kPre];
-    load_geoms<HEADERS>(f, n, g, fl, start, d, flags);
-    if (total > cap || st != 0) return;
-    const FrameWords w = frame_words(g[0], (total + 15) >> 4);
-    const uint64_t head_f = w.ilo - w.olo, tail = w.ohi - w.ihi;
-    uint64_t word;
-    if (q < head_f) word = w.olo + q;
-    else if (q < head_f + tail) word = w.ihi + (q - head_f);
-    else return;
-    edge[f64 * kEdgeWords + q] = compose_word<HEADERS>(16u * word, f, n, g, fl, src, start, d, flags);
-}
+// A frame's unit geometry for the slot-parallel record pass (LDS), word
+// indices relative to its first unit base b0.
+struct FrameUnits {
+    uint64_t b0, sdel;
+    uint32_t olo, ohi, ilo, ihi;  // owned and interior words - b0
+    uint32_t rk, units, head_f, nedge;
+};
 
-#ifndef KMWS_REC_EDGE_WAVES
-#define KMWS_REC_EDGE_WAVES 1  // min waves per SIMD the register budget must allow (tuning)
-#endif
-// Unit records and edge words in one grid (they are independent, and the
-// record blocks alone are too few to fill the chip): virtual block v < rec_blocks
-// writes records (record block rec_lo + v), v >= rec_blocks composes edge words
-// (edge block edge_lo + v - rec_blocks); v = vbase + blockIdx.x, the grid being
-// cut at 2^31 work-items per launch.  A frame chunk of the pack pipeline passes
-// the record and edge blocks it owns (launch_copy: each block in one chunk).
+// Everything the copy waves need of 256 frames, one block:
+//   edge words -- a frame's owned words outside its interior: q < head_f at
+//     olo + q, then the tail at ihi + (q - head_f) -- one thread per frame,
+//     into LDS, then written out over one contiguous run edge[F0 * kEdgeWords ...]
+//     (coalesced; 128-byte lines without a live word are skipped);
+//   unit records, slot-parallel: slot s of the block finds its frame by a
+//     binary search over the block's slot bases in LDS (slots past a frame's
+//     exact unit count are marked empty); consecutive threads write
+//     consecutive records.
+// Edge words: the head word (q = 0 if head_f) holds the frame's header end and
+// first payload bytes; the tail words (q = head_f + i) hold its last payload
+// bytes (i = 0 only), then frame f+1's header and payload.  Every source word
+// is loaded before anything is composed (one latency level): frame f's words
+// of the head and first tail word, and a window of 5 consecutive source words
+// of frame f+1 from which every tail word funnels its payload bytes (window
+// indices clamped to f+1's payload; clamped words only feed bytes outside it,
+// which are masked off).  The rare word a third region reaches into (a frame
+// ending inside it) is composed byte by byte.  Also the capacity check (status
+// set if the output exceeds cap; nothing is written then).
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock, KMWS_REC_EDGE_WAVES) rec_edge_kernel(const uint8_t* __restrict__ src,
+__global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
                                                           const uint64_t* __restrict__ start,
                                                           const uint64_t* __restrict__ ubase,
                                                           const kmws_desc* __restrict__ d,
                                                           const uint16_t* __restrict__ flags, uint32_t n,
                                                           uint64_t cap, UnitRec* __restrict__ rec,
                                                           u32x4* __restrict__ edge, WsHead* __restrict__ head,
-                                                          uint64_t rec_lo, uint64_t rec_blocks, uint64_t edge_lo,
-                                                          uint64_t vbase)
+                                                          uint64_t f_lo, uint64_t f_hi)
 {
+    __shared__ FrameUnits s_fu[kBlock];
     __shared__ uint32_t s_ub[kBlock + 1];
-    const uint64_t v = vbase + blockIdx.x;
-    if (v < rec_blocks)
-        unit_rec_block<HEADERS>((uint32_t)(rec_lo + v), s_ub, start, ubase, d, flags, n, cap, rec, head);
-    else
-        edge_block<HEADERS>(edge_lo + (v - rec_blocks), src, start, d, flags, n, cap, edge, head);
+    __shared__ u32x4 s_edge[kBlock * kEdgeWords];
+    __shared__ uint8_t s_ne[kBlock];  // live edge words per frame
+    const uint64_t F0 = f_lo + (uint64_t)blockIdx.x * kBlock;
+    const uint32_t nf = f_hi - F0 < (uint64_t)kBlock ? (uint32_t)(f_hi - F0) : (uint32_t)kBlock;
+    const uint32_t t = threadIdx.x;
+    // total, slot bases and the three frames' geometry: one latency level
+    const uint64_t total = start[n];
+    const uint64_t S0 = ubase[F0];
+    const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
+    const uint64_t uf = ubase[f], uend = ubase[F0 + nf];
+    FrameGeom g[kPre];
+    uint32_t fl[kPre];
+    load_geoms<HEADERS>(f, n, g, fl, start, d, flags);
+    if (total > cap) {  // records would not fit the workspace; the copy waves see the status (block-uniform)
+        if (F0 == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    if (t < nf) {
+        const FrameWords w = frame_words(g[0], (total + 15) >> 4);
+        uint32_t head_f = (uint32_t)(w.ilo - w.olo);
+        uint32_t nedge = head_f + (uint32_t)(w.ohi - w.ihi);
+        if (nedge > (uint32_t)kEdgeWords || w.olo - w.b0 >= kUnitAlign) {  // cannot happen
+            atomicOr(&head->status, kStatusBadDesc);
+            nedge = head_f = 0;
+        }
+        s_ub[t] = (uint32_t)(uf - S0);
+        if (t == nf - 1) s_ub[nf] = (uint32_t)(uend - S0);
+        FrameUnits fu;
+        fu.b0 = w.b0;
+        fu.sdel = g[0].sdel;
+        fu.olo = (uint32_t)(w.olo - w.b0);
+        fu.ohi = (uint32_t)(w.ohi - w.b0);
+        fu.ilo = (uint32_t)(w.ilo - w.b0);
+        fu.ihi = (uint32_t)(w.ihi - w.b0);
+        fu.rk = g[0].key ? rot_key(g[0].key, g[0].p0) : 0u;
+        fu.units = (uint32_t)w.units;
+        fu.head_f = head_f;
+        fu.nedge = nedge;
+        s_ne[t] = (uint8_t)nedge;
+        s_fu[t] = fu;
+
+        const FrameGeom& F = g[0];
+        const FrameGeom& N = g[1];
+        const uint32_t ntail = nedge - head_f;
+        const uint64_t ah = 16u * w.olo, at = 16u * w.ihi;
+        u32x4 H0, H1, T0, T1, S[kLineWords + 1];
+        pay_words(head_f != 0 && nedge != 0, F, ah, src, H0, H1);
+        pay_words(ntail != 0, F, at, src, T0, T1);
+        const bool nlive = ntail != 0 && N.r0 < at + 16 * kLineWords && N.r1 > N.p0;
+        const uint64_t soff = N.p0 + N.sdel;  // f+1's source offset
+        const int64_t wb = (int64_t)(at + N.sdel) >> 4, wlo = (int64_t)(soff >> 4),
+                      whi = (int64_t)((soff + N.len - 1) >> 4);
+        const uint32_t delta = (uint32_t)((at + N.sdel) & 15u);
+#pragma unroll
+        for (int j = 0; j <= (int)kLineWords; ++j) {
+            int64_t k = wb + j;
+            k = k < wlo ? wlo : (k > whi ? whi : k);
+            S[j] = *reinterpret_cast<const u32x4*>(src + (nlive ? 16 * (uint64_t)k : 0));
+        }
+        u32x4* my = s_edge + t * kEdgeWords;
+        uint32_t third = 0;
+        if (head_f && nedge) {
+            if (F.r1 < ah + 16 && (uint64_t)f + 1 < n) {
+                third |= 1u;
+            } else {
+                u32x4 out = u32x4{0, 0, 0, 0};
+                put_frame<HEADERS>(out, ah, F, fl[0], H0, H1);
+                my[0] = out;
+            }
+        }
+        const uint32_t rkN = N.key ? rot_key(N.key, N.p0) : 0u;
+#pragma unroll
+        for (int i = 0; i < (int)kLineWords; ++i) {
+            const uint64_t a = at + 16u * i;
+            const uint32_t q = head_f + i;
+            if ((uint32_t)i >= ntail) break;
+            if (N.r0 < a + 16 && N.r1 < a + 16 && (uint64_t)f + 2 < n) {
+                third |= 1u << q;
+                continue;
+            }
+            u32x4 out = u32x4{0, 0, 0, 0};
+            if (i == 0) put_frame<HEADERS>(out, a, F, fl[0], T0, T1);
+            if (N.r0 < a + 16) {
+                if (HEADERS && N.p0 > a && N.p0 > N.r0) {  // f+1's header bytes [r0, p0)
+                    uint64_t h0, h1;
+                    build_header(N.len, fl[1], N.key, h0, h1);
+                    const int sh = (int)((int64_t)N.r0 - (int64_t)a);
+                    const u32x4 Hw = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+                    const int he = (int)(N.p0 - N.r0) + sh;
+                    out |= shift_in(Hw, sh) & byte_range(sh < 0 ? 0 : sh, he > 16 ? 16 : he);
+                }
+                if (N.r1 > N.p0 && N.p0 < a + 16 && N.r1 > a) {  // f+1's payload bytes
+                    const uint64_t lo_b = N.p0 > a ? N.p0 : a, hi_b = N.r1 < a + 16 ? N.r1 : a + 16;
+                    out |= (funnel16(S[i], S[i + 1], delta) ^ rkN) & byte_range((int)(lo_b - a), (int)(hi_b - a));
+                }
+            }
+            my[q] = out;
+        }
+#pragma clang loop unroll(disable)
+        for (int q = 0; third != 0; ++q, third >>= 1) {
+            if (third & 1u) {
+                const uint64_t a = 16u * ((uint32_t)q < head_f ? w.olo + q : w.ihi + (q - head_f));
+                my[q] = compose_word_bytes<HEADERS>(a, f, n, src, start, d, flags);
+            }
+        }
+    }
+    __syncthreads();
+    // edge words of the block's frames: one contiguous run, whole 128-byte lines
+    // (the run starts on one: 256 frames x 80 B), skipping lines without a live
+    // word (a line written in part costs more than writing it whole)
+    u32x4* eout = edge + F0 * kEdgeWords;
+    const uint32_t nw = nf * (uint32_t)kEdgeWords;
+    for (uint32_t i = t; i < nw; i += kBlock) {
+        // the line [l0, l0 + 8) meets frames j0..j1 (at most 3); frame j's live
+        // words are [5j, 5j + nedge_j), and every frame after j0 starts inside the line
+        const uint32_t l0 = i & ~7u, j0 = l0 / kEdgeWords, j1 = (l0 + 7) / kEdgeWords;
+        bool live = kEdgeWords * j0 + s_ne[j0] > l0;
+        if (j0 + 1 < nf && j0 + 1 <= j1) live |= s_ne[j0 + 1] != 0;
+        if (j0 + 2 < nf && j0 + 2 <= j1) live |= s_ne[j0 + 2] != 0;
+        if (live) eout[i] = s_edge[i];  // dead words of a live line: any value (never read)
+    }
+    // unit records, slot-parallel
+    const uint32_t ns = s_ub[nf];
+    for (uint32_t sl = t; sl < ns; sl += kBlock) {
+        uint32_t lo = 0, hi = nf;  // s_ub[lo] <= sl < s_ub[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_ub[mid] <= sl) lo = mid; else hi = mid;
+        }
+        const FrameUnits fu = s_fu[lo];
+        const uint32_t m = sl - s_ub[lo];
+        UnitRec r;
+        if (m < fu.units) {
+            const uint32_t b = m * (uint32_t)kUnitWords;  // unit base - b0
+            auto rel = [&](uint32_t x) -> uint32_t {
+                return x <= b ? 0u : (x - b >= (uint32_t)kUnitWords ? (uint32_t)kUnitWords : x - b);
+            };
+            r.dst = 16u * (fu.b0 + b);
+            r.src = 16u * (fu.b0 + b) + fu.sdel;
+            r.f = (uint32_t)F0 + lo;
+            r.rk = fu.rk;
+            const uint32_t klo = rel(fu.olo), khi = rel(fu.ohi), ilo = rel(fu.ilo), ihi = rel(fu.ihi);
+            r.own = klo | fu.head_f << 12 | khi << 16;
+            r.inner = ilo | ihi << 16;
+            if (ilo - klo > fu.head_f)  // cannot happen
+                atomicOr(&head->status, kStatusBadDesc);
+        } else {
+            r.dst = r.src = 0;
+            r.f = r.rk = 0;
+            r.own = r.inner = 0;
+        }
+        rec[S0 + sl] = r;
+    }
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
@@ -942,11 +1016,12 @@ static uint64_t max_units(uint32_t n, uint64_t cap)
     return (u + kBlock / 64 - 1) / (kBlock / 64) * (kBlock / 64);
 }
 static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
+static uint64_t r256(uint64_t x) { return (x + 255) & ~255ull; }
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8) +
-           (uint64_t)n * kEdgeWords * 16 + max_units(n, cap) * sizeof(UnitRec);
+    return r256(sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8)) +
+           r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -959,8 +1034,9 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     p += r16((n_scan_blocks(n) + 1) * sizeof(V2));
     c.ubase = reinterpret_cast<uint64_t*>(p);
     p += r16(((uint64_t)n + 1) * 8);
+    p = static_cast<char*>(ws) + r256(p - static_cast<char*>(ws));  // edge words and records on whole lines
     c.edge = reinterpret_cast<u32x4*>(p);
-    p += (uint64_t)n * kEdgeWords * 16;
+    p += r256((uint64_t)n * kEdgeWords * 16);
     c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
 }
@@ -1022,8 +1098,14 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
                                const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t fb = (n + kBlock - 1) / kBlock;
-    const uint64_t eb = ((uint64_t)n + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock;
-    constexpr uint64_t kMaxBlocks = (1ull << 31) / kBlock;  // stay below 2^31 work-items per launch
+    constexpr uint64_t kMaxFrames = (1ull << 31) - kBlock;  // stay below 2^31 work-items per launch
+    auto prologue = [&](uint64_t F0, uint64_t F1, hipStream_t st) {  // records + edge words of frames [F0, F1)
+        for (uint64_t f0 = F0; f0 < F1; f0 += kMaxFrames) {
+            const uint64_t f1 = F1 - f0 < kMaxFrames ? F1 : f0 + kMaxFrames;
+            hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)((f1 - f0 + kBlock - 1) / kBlock)), dim3(kBlock),
+                               0, st, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head, f0, f1);
+        }
+    };
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
     // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
     // batches of small frames need every wave slot to hide their per-unit
@@ -1046,10 +1128,7 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
     const uint32_t K = pack_chunks(n);
     if (K == 1) {
-        for (uint64_t v0 = 0, nv = fb + eb; v0 < nv; v0 += kMaxBlocks)
-            hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
-                               dim3(kBlock), 0, s, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
-                               (uint64_t)0, (uint64_t)fb, (uint64_t)0, v0);
+        prologue(0, n, s);
         for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
             const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
             hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
@@ -1058,16 +1137,12 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
         }
         return hip_status(hipGetLastError());
     }
-    // Pipeline: the record/edge grids of the K frame chunks run back to back on a
+    // Pipeline: the prologue grids of the K frame chunks run back to back on a
     // side stream while the copy grid of chunk j (caller's stream) waits only for
-    // chunk j's records, so all but the first chunk's prologue hides under copies.
+    // chunk j's prologue, so all but the first chunk's prologue hides under copies.
     // Fork and join are events, so the call stays stream-ordered and capturable.
-    // Chunk boundaries are whole record blocks (F_j = 256 R_j), and each edge
-    // block belongs to the chunk holding its first frame (blocks
-    // [ceil(F_j / 51), ceil(F_j+1 / 51))): every record and edge block is
-    // written exactly once, and chunk j's copy (which waits for the grids of
-    // chunks 0..j, issued in order on one stream) needs no block of a later
-    // chunk -- no grid writes what a running copy grid reads.
+    // A unit reads only its own frame's record and edge words, each written by
+    // that frame's prologue thread: no grid writes what a running copy grid reads.
     PackSide* ps = pack_side();
     if (!ps) return KMWS_ERR_FAILED;
     if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->ss, ps->fork, 0) != hipSuccess)
@@ -1076,15 +1151,8 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, c
         const uint64_t f = (uint64_t)kBlock * ((uint64_t)fb * j / K);
         return f < n ? f : n;
     };
-    auto edge_blk = [](uint64_t f) { return (f + kEdgeFramesPerBlock - 1) / kEdgeFramesPerBlock; };
     for (uint32_t j = 0; j < K; ++j) {
-        const uint64_t F0 = chunk_frame(j), F1 = chunk_frame(j + 1);
-        const uint64_t r0 = F0 / kBlock, r1 = (F1 + kBlock - 1) / kBlock;
-        const uint64_t e0 = edge_blk(F0), e1 = edge_blk(F1);
-        for (uint64_t v0 = 0, nv = (r1 - r0) + (e1 - e0); v0 < nv; v0 += kMaxBlocks)
-            hipLaunchKernelGGL(rec_edge_kernel<HEADERS>, dim3((uint32_t)(nv - v0 < kMaxBlocks ? nv - v0 : kMaxBlocks)),
-                               dim3(kBlock), 0, ps->ss, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head,
-                               r0, r1 - r0, e0, v0);
+        prologue(chunk_frame(j), chunk_frame(j + 1), ps->ss);
         if (hipEventRecord(ps->ev[j], ps->ss) != hipSuccess) return KMWS_ERR_FAILED;
     }
     uint64_t gw = (units + K - 1) / K;  // waves per chunk grid (equal chunks: one unit each)
