@@ -54,6 +54,13 @@ inline kmws_status hip_status(hipError_t e)
     return e == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
 }
 
+// Zeroes `bytes` (a multiple of 8, at most 4 KiB) at an 8-byte aligned device
+// address with one small kernel.  Used instead of hipMemsetAsync for the status
+// word and scan totals: a call captured into a HIP graph then holds kernel nodes
+// only (replayed memset nodes of this runtime were seen writing a pointer value
+// instead of zero when the graph was replayed after other work on the device).
+kmws_status launch_zero(void* p, uint32_t bytes, hipStream_t s);
+
 // Small host batches (the decoder's staging, kmws_unmask.hip): one block per
 // piece of at most kPieceWords 16-byte words of one frame's aligned hull.
 constexpr uint32_t kPieceWords = 4 * kBlock;  // 16 KiB

@@ -1047,8 +1047,8 @@ static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, 
 {
     const uint32_t nb = (uint32_t)n_scan_blocks(n);
     if (nb == 0) {
-        if (hipMemsetAsync(out, 0, sizeof(uint64_t), s) != hipSuccess) return KMWS_ERR_FAILED;
-        return hip_status(hipMemsetAsync(c.ubase, 0, sizeof(uint64_t), s));
+        if (launch_zero(out, sizeof(uint64_t), s) != KMWS_OK) return KMWS_ERR_FAILED;
+        return launch_zero(c.ubase, sizeof(uint64_t), s);
     }
     hipLaunchKernelGGL(scan_reduce_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials);
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kBlock), 0, s, c.partials, nb, out + n, c.ubase + n);
@@ -1186,7 +1186,7 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    if (hipMemsetAsync(c.head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
+    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     kmws_status st = launch_scan(WireSize{descs, flags}, n, wire_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<true>(src, dst, dst_cap, wire_off, descs, flags, n, c, s);
@@ -1202,7 +1202,7 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    if (hipMemsetAsync(c.head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
+    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
@@ -1219,7 +1219,7 @@ kmws_status kmws_unpack_headers(const uint8_t* wire, uint64_t wire_len, const ui
         (mode != KMWS_MODE_CLIENT && mode != KMWS_MODE_SERVER))
         return KMWS_ERR_INVALID_PARAM;
     WsHead* head = static_cast<WsHead*>(workspace);
-    if (hipMemsetAsync(head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
+    if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     if (n == 0) return KMWS_OK;
     hipLaunchKernelGGL(unpack_headers_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, wire, wire_len,
                        hdr_off, n, mode, out_desc, out_flags, out_err, head);

@@ -454,7 +454,7 @@ static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n
     kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
     if (st != KMWS_OK) return st;
     WsHead* head = static_cast<WsHead*>(workspace);
-    if (hipMemsetAsync(head, 0, sizeof(WsHead), s) != hipSuccess) return KMWS_ERR_FAILED;
+    if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     if (n == 0 || span == 0) return KMWS_OK;
     hipLaunchKernelGGL(tile_map_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, n, span,
                        ilog2_u64(UnmaskCfg<V>::kTile), reinterpret_cast<uint32_t*>(head + 1), head);
@@ -603,6 +603,18 @@ static uint32_t current_schedule()
 static bool bad_args(const uint8_t* base, const kmws_desc* descs, uint32_t n, const void* ws)
 {
     return !ws || (n && (!base || !descs)) || (reinterpret_cast<uintptr_t>(base) & 15u);
+}
+
+__global__ void __launch_bounds__(64) zero_kernel(uint64_t* __restrict__ p, uint32_t words)
+{
+    for (uint32_t i = threadIdx.x; i < words; i += 64) p[i] = 0;
+}
+
+kmws_status launch_zero(void* p, uint32_t bytes, hipStream_t s)
+{
+    if (!p || (bytes & 7u) || bytes > 4096) return KMWS_ERR_INVALID_PARAM;
+    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(64), 0, s, static_cast<uint64_t*>(p), bytes / 8);
+    return hip_status(hipGetLastError());
 }
 
 kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,

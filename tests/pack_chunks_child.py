@@ -1,6 +1,6 @@
 """Child process of tests/test_gpu_pack.py::test_pack_chunks_knob: the library
-reads KMWS_PACK_CHUNKS once per process, so the chunked pack pipeline (record /
-edge grids on a side stream under per-chunk copy grids) is checked here, with
+reads KMWS_PACK_CHUNKS once per process, so the chunked pack pipeline (prologue
+grids on a side stream under per-chunk copy grids) is checked here, with
 the knob set by the parent.  Encode and gather-unmask of several layouts, each
 compared byte for byte with the oracle; exit status 0 = all equal."""
 import os
