@@ -271,6 +271,23 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
                               uint8_t* dst, uint64_t dst_cap, uint64_t* wire_off, void* workspace,
                               size_t workspace_bytes, void* stream);
 
+/* Workspace bytes for kmws_pack_headers with n frames. */
+size_t kmws_pack_headers_workspace_size(uint32_t n);
+
+/* Batched header pack only -- the device form of kuma's send iovec
+ * {header, payload} (WebSocketImpl.cpp:381-404, :419-431): frame i's header,
+ * WSHandler::encodeFrameHeader (WSHandler.cpp:46-106) of {flags[i],
+ * descs[i].len, descs[i].key}, is written to the 16-byte slot hdr + 16 i (its
+ * hdr_len[i] = 2..14 bytes first, the rest of the slot zero).  The payloads are
+ * not touched: mask them in place with kmws_unmask_batch on the same
+ * descriptors (XOR is its own inverse), as sendWsFrame masks the caller's
+ * buffer (:388).  wire_off (n+1 entries, may be NULL) receives the offsets the
+ * frames would have back to back on the wire (exclusive scan of header +
+ * payload bytes) and the total in wire_off[n].  hdr 16-B aligned. */
+kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
+                              uint8_t* hdr_len, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
 /* Workspace bytes for kmws_unpack_headers. */
 size_t kmws_unpack_workspace_size(void);
 

@@ -107,6 +107,7 @@ __host__ __device__ __forceinline__ uint64_t unit_bound(uint64_t R)
 }
 
 struct WireSize {
+    static constexpr bool kHeaders = true;
     const kmws_desc* d;
     const uint16_t* flags;
     __device__ V2 operator()(uint32_t f) const
@@ -117,6 +118,7 @@ struct WireSize {
     }
 };
 struct PayloadSize {
+    static constexpr bool kHeaders = false;
     const kmws_desc* d;
     __device__ V2 operator()(uint32_t f) const
     {
@@ -199,9 +201,12 @@ __global__ void __launch_bounds__(kBlock) scan_partials_kernel(V2* __restrict__ 
     }
 }
 
+// (hdr != nullptr: also frame f's header bytes into the 16-byte slot hdr[f] and
+// its length into hl_out[f] -- kmws_pack_headers; Size is WireSize then)
 template <class Size>
 __global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n, const V2* __restrict__ partials,
-                                                           uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b)
+                                                           uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b,
+                                                           u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
 {
     __shared__ V2 s_row[kScanItems][kBlock / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -231,6 +236,16 @@ __global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n
         if (f < n) {
             out_a[f] = run.a + before.a + ex[i].a;
             out_b[f] = run.b + before.b + ex[i].b;
+            if constexpr (Size::kHeaders) {
+                if (hdr) {
+                    const kmws_desc x = size.d[f];
+                    const uint32_t fl = size.flags[f];
+                    uint64_t h0, h1;
+                    build_header(x.len, fl, x.key, h0, h1);
+                    hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+                    if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
+                }
+            }
         }
         run = run + row;
     }
@@ -997,6 +1012,23 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
     if (out_err) out_err[f] = err;
 }
 
+// ------------------------------ header pack only ------------------------------
+// One lane per frame: the header bytes of WSHandler::encodeFrameHeader in a
+// 16-byte slot (one coalesced store per lane) and its length.
+__global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* __restrict__ d,
+                                                              const uint16_t* __restrict__ flags, uint32_t n,
+                                                              u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
+{
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n) return;
+    const kmws_desc x = d[f];
+    const uint32_t fl = flags[f];
+    uint64_t h0, h1;
+    build_header(x.len, fl, x.key, h0, h1);
+    hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+    if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
+}
+
 // ------------------------------ host launchers ------------------------------
 struct CopyWs {
     WsHead* head;
@@ -1043,7 +1075,8 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
 
 // Region offsets -> out (n+1 entries), unit slot bases -> c.ubase (n+1 entries).
 template <class Size>
-static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s)
+static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s, u32x4* hdr = nullptr,
+                               uint8_t* hl_out = nullptr)
 {
     const uint32_t nb = (uint32_t)n_scan_blocks(n);
     if (nb == 0) {
@@ -1052,7 +1085,8 @@ static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, 
     }
     hipLaunchKernelGGL(scan_reduce_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials);
     hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kBlock), 0, s, c.partials, nb, out + n, c.ubase + n);
-    hipLaunchKernelGGL(scan_emit_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials, out, c.ubase);
+    hipLaunchKernelGGL(scan_emit_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials, out, c.ubase, hdr,
+                       hl_out);
     return hip_status(hipGetLastError());
 }
 
@@ -1206,6 +1240,40 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
     kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
+}
+
+// scan partials + scratch unit bases after the status word (the scan's second
+// quantity is not needed here but costs nothing)
+size_t kmws_pack_headers_workspace_size(uint32_t n)
+{
+    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8);
+}
+
+kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
+                              uint8_t* hl_out, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
+                              void* stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if ((n && (!descs || !flags || !hdr)) || (reinterpret_cast<uintptr_t>(hdr) & 15u) ||
+        (wire_off && !workspace))
+        return KMWS_ERR_INVALID_PARAM;
+    if (wire_off) {
+        if (workspace_bytes < kmws_pack_headers_workspace_size(n)) return KMWS_ERR_BUFFER_TOO_SMALL;
+        char* p = static_cast<char*>(workspace);
+        CopyWs c;
+        c.head = reinterpret_cast<WsHead*>(p);
+        c.partials = reinterpret_cast<V2*>(p + sizeof(WsHead));
+        c.ubase = reinterpret_cast<uint64_t*>(p + sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)));
+        c.rec = nullptr;
+        c.edge = nullptr;
+        if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+        // the scan's emit pass writes the header slots too
+        return launch_scan(WireSize{descs, flags}, n, wire_off, c, s, reinterpret_cast<u32x4*>(hdr), hl_out);
+    }
+    if (n == 0) return KMWS_OK;
+    hipLaunchKernelGGL(pack_headers_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, flags, n,
+                       reinterpret_cast<u32x4*>(hdr), hl_out);
+    return hip_status(hipGetLastError());
 }
 
 size_t kmws_unpack_workspace_size(void) { return sizeof(WsHead); }

@@ -34,6 +34,7 @@ EXPORTS = [
     "kmws_unmask_batch_variant", "kmws_unmask_autotune", "kmws_unmask_schedule", "kmws_unmask_resident_blocks", "kmws_read_status", "kmws_fill_synthetic",
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
+    "kmws_pack_headers_workspace_size", "kmws_pack_headers",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
@@ -111,6 +112,8 @@ def lib() -> C.CDLL:
         "kmws_copy_workspace_size": (sz, [u32, u64]),
         "kmws_encode_batch": (i32, [u8p, vp, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_unpack_workspace_size": (sz, []),
+        "kmws_pack_headers_workspace_size": (sz, [u32]),
+        "kmws_pack_headers": (i32, [vp, vp, u32, u8p, vp, vp, vp, sz, vp]),
         "kmws_unpack_headers": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, vp]),
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
@@ -534,6 +537,22 @@ def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None) -
     _check(lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), flags.data_ptr(), descs.shape[0],
                                    dst.data_ptr(), dst.numel(), wire_off.data_ptr(), ws.ptr, ws.nbytes,
                                    _stream_handle(stream)), "kmws_encode_batch")
+
+
+def pack_headers_workspace_size(n: int) -> int:
+    return lib().kmws_pack_headers_workspace_size(n)
+
+
+def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Workspace] = None,
+                 stream=None) -> None:
+    """kmws_pack_headers: headers only, frame i's into the 16-B slot hdr[16 i:]
+    (uint8 device tensor of >= 16 n bytes), lengths into hdr_len (uint8, n),
+    wire offsets into wire_off (int64, n+1; needs ws)."""
+    _check(lib().kmws_pack_headers(descs.data_ptr(), flags.data_ptr(), descs.shape[0], hdr.data_ptr(),
+                                   hdr_len.data_ptr() if hdr_len is not None else None,
+                                   wire_off.data_ptr() if wire_off is not None else None,
+                                   ws.ptr if ws is not None else None, ws.nbytes if ws is not None else 0,
+                                   _stream_handle(stream)), "kmws_pack_headers")
 
 
 def unpack_headers(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: Workspace,

@@ -227,6 +227,59 @@ def test_unpack_quirk127_lengths(T):
         assert int(out_desc.cpu().numpy()[0, 1] & 0xFFFFFFFF) == L
 
 
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "max", "tiny"])
+def test_pack_headers_parity(T, kind):
+    """kmws_pack_headers: every 16-B slot == the oracle's encodeFrameHeader bytes
+    (zero-padded), lengths and wire offsets == the oracle's encode_batch; the
+    payloads masked in place by kmws_unmask_batch on the same descriptors then
+    equal the oracle wire image's payload bytes (kuma's iovec {hdr, payload})."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(zlib.crc32(f"pack-headers-{kind}".encode()))
+    n = 300 if kind != "max" else 6
+    lens, flags, keys = frames(rng, kind, n)
+    src, offs = src_arena(rng, lens, True)
+    want, want_off = orc.encode_batch(src, offs, lens, flags, keys)
+    descs = kmws.make_descs(offs.astype(np.int64), lens, keys.astype(np.int64))
+    fl = T.from_numpy(flags.astype(np.int16)).cuda()
+    hdr = T.full((16 * n,), 0xEE, dtype=T.uint8, device="cuda")
+    hl = T.zeros(n, dtype=T.uint8, device="cuda")
+    woff = T.zeros(n + 1, dtype=T.int64, device="cuda")
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    kmws.pack_headers(descs, fl, hdr, hl, woff, ws)
+    T.cuda.synchronize()
+    assert ws.status() == 0
+    H = hdr.cpu().numpy().reshape(n, 16)
+    L = hl.cpu().numpy()
+    wo = woff.cpu().numpy()
+    for i in range(n):
+        m = bool(flags[i] >> 8 & 1)
+        want_h = orc.encode_header(orc.Hdr(fin=int(flags[i] >> 7 & 1), rsv1=int(flags[i] >> 6 & 1),
+                                           rsv2=int(flags[i] >> 5 & 1), rsv3=int(flags[i] >> 4 & 1),
+                                           opcode=int(flags[i] & 15), mask=int(m),
+                                           maskey=int(keys[i]).to_bytes(4, "little"), length=int(lens[i])))
+        assert int(L[i]) == len(want_h), i
+        assert bytes(H[i]) == want_h + bytes(16 - len(want_h)), i
+        assert int(wo[i]) == int(want_off[i]), i
+        assert bytes(want[int(wo[i]):int(wo[i]) + len(want_h)]) == want_h
+    assert int(wo[n]) == len(want)
+    # payloads masked in place with the same descriptors (masked frames only carry a key)
+    d_src = to_dev(T, src)
+    mk = np.where((flags >> 8) & 1, keys, 0).astype(np.int64)
+    d2 = kmws.make_descs(offs.astype(np.int64), lens, mk)
+    wsm = kmws.Workspace(kmws.unmask_workspace_size(len(src)))
+    kmws.unmask_batch(d_src, d2, wsm, len(src))
+    T.cuda.synchronize()
+    got = d_src.cpu().numpy()
+    for i in range(n):
+        p0 = int(wo[i]) + int(L[i])
+        assert bytes(got[int(offs[i]):int(offs[i]) + int(lens[i])]) == bytes(want[p0:p0 + int(lens[i])]), i
+    # headers only, no offsets (no workspace)
+    hdr2 = T.zeros((16 * n,), dtype=T.uint8, device="cuda")
+    kmws.pack_headers(descs, fl, hdr2)
+    T.cuda.synchronize()
+    assert T.equal(hdr2, hdr)
+
+
 @pytest.mark.parametrize("chunks", [3, 8])
 def test_pack_chunks_knob(T, chunks):
     """The chunked pack pipeline (KMWS_PACK_CHUNKS, read once per process) in a

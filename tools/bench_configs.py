@@ -349,6 +349,13 @@ def cfg4(reps: int, messages: int):
     ws_e = kmws.Workspace(kmws.copy_workspace_size(n, wire.numel()))
     t_pack = timed(torch, lambda: kmws.encode_batch(src, descs, fl16, wire, wire_off, ws_e), reps)
     assert ws_e.status() == 0 and int(wire_off[n]) == P + H
+    # headers only (kmws_pack_headers: 16-B slots + lengths + wire offsets), the iovec send form
+    hslots = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    hlen = torch.empty(n, dtype=torch.uint8, device=dev)
+    woff2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ws_h = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    t_hdr = timed(torch, lambda: kmws.pack_headers(descs, fl16, hslots, hlen, woff2, ws_h), reps)
+    assert torch.equal(woff2, wire_off) and torch.equal(hslots.view(n, 16)[:, :8], wire[:P + H].view(n, L + 8)[:, :8])
     out_desc = torch.empty((n, 2), dtype=torch.int64, device=dev)
     out_flags = torch.empty(n, dtype=torch.int16, device=dev)
     out_err = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -376,6 +383,9 @@ def cfg4(reps: int, messages: int):
     return {"config": "cfg4", "messages": messages, "frames": n, "payload_bytes": P,
             "pack": {"ms": t_pack * 1e3, "Mheaders_s": n / t_pack / 1e6, "payload_GiB_s": P / t_pack / 2**30,
                      "hbm_frac": (2 * P + H + 26 * n) / t_pack / 8e12},
+            "pack_headers_only": {"ms": t_hdr * 1e3, "Mheaders_s": n / t_hdr / 1e6,
+                                  # desc 16 + flags 2 in, slot 16 + length 1 + wire offset 8 out
+                                  "hbm_frac": 43 * n / t_hdr / 8e12},
             "unpack": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
             "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30,
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
