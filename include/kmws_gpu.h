@@ -319,6 +319,20 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
 kmws_status kmws_find_headers(const uint8_t* wire, uint64_t len, uint64_t* hdr_off, uint32_t cap,
                               uint32_t* n_out, uint64_t* consumed);
 
+/* Device: the same header-chain walk as kmws_find_headers, one lane per
+ * stream, for many streams at once (boundary discovery is serial within a
+ * stream -- frame k+1 starts where frame k's header says -- so a batch gets its
+ * parallelism from connections; SURVEY 8 "hard parts").  Stream s is
+ * wire[stream_off[s] .. stream_off[s+1]) (stream_off: n_streams+1 ascending
+ * entries, stream_off[n_streams] <= wire_len).  Its header offsets (absolute,
+ * into wire) go to hdr_off[s * cap .. s * cap + n_out[s]); consumed[s] (may be
+ * NULL) = bytes of stream s covered by its complete frames.  Stopping rules as
+ * kmws_find_headers: cap frames, a truncated frame or invalid length (recorded),
+ * or after a CLOSE frame.  All pointers device memory. */
+kmws_status kmws_find_headers_streams(const uint8_t* wire, uint64_t wire_len, const uint64_t* stream_off,
+                                      uint32_t n_streams, uint64_t* hdr_off, uint32_t cap, uint32_t* n_out,
+                                      uint64_t* consumed, void* stream);
+
 /* ---- host-resident batches: pinned H2D -> kernel -> D2H pipeline ---- */
 typedef struct kmws_pipeline kmws_pipeline;
 

@@ -1029,6 +1029,68 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
     if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
 }
 
+// ------------------------------ header-chain walk, many streams ------------------------------
+// One lane per stream, the rules of kmws_find_headers (kmws_codec.cpp) /
+// the header states of WSHandler::decodeFrame (WSHandler.cpp:118-197): each
+// step reads the (at most 10) bytes it needs from one pair of aligned 16-byte
+// loads (byte loads near the wire's end), decodes the length class (with the
+// 127-class shift quirk) and jumps over the payload.
+__global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __restrict__ wire, uint64_t wire_len,
+                                                              const uint64_t* __restrict__ stream_off,
+                                                              uint32_t n_streams, uint64_t* __restrict__ hdr_off,
+                                                              uint32_t cap, uint32_t* __restrict__ n_out,
+                                                              uint64_t* __restrict__ consumed)
+{
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n_streams) return;
+    const uint64_t lo = stream_off[s], hi = stream_off[s + 1];
+    const uintptr_t end16 = (reinterpret_cast<uintptr_t>(wire) + wire_len + 15) & ~(uintptr_t)15;
+    uint64_t* out = hdr_off + (uint64_t)s * cap;
+    uint64_t p = lo, done = lo;
+    uint32_t n = 0;
+    while (p < hi && n < cap) {
+        out[n++] = p;
+        if (p + 2 > hi) break;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(wire + p), a16 = a & ~(uintptr_t)15;
+        u32x4 hw = u32x4{0, 0, 0, 0};
+        if (a16 + 32 <= end16) {
+            hw = funnel16(*reinterpret_cast<const u32x4*>(a16), *reinterpret_cast<const u32x4*>(a16 + 16),
+                          (uint32_t)(a & 15u));
+        } else {
+            const uint64_t avail = hi - p < 10 ? hi - p : 10;
+            for (uint32_t k = 0; k < (uint32_t)avail; ++k) {
+                const uint32_t b = wire[p + k], sh = 8u * (k & 3u);
+                if ((k >> 2) == 0) hw.x |= b << sh;
+                else if ((k >> 2) == 1) hw.y |= b << sh;
+                else hw.z |= b << sh;
+            }
+        }
+        const uint32_t b0 = hw.x & 0xFFu, b1 = (hw.x >> 8) & 0xFFu;
+        const uint32_t plen = b1 & 0x7F, mask = b1 >> 7;
+        const uint64_t ext = plen == 126 ? 2 : (plen == 127 ? 8 : 0);
+        if (p + 2 + ext > hi) break;
+        uint64_t L;
+        if (plen == 126) {
+            L = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
+        } else if (plen == 127) {
+            uint64_t x = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << (((7u - k) * 8u) & 31u));
+            if ((x >> 63) != 0 || (uint32_t)x > KMWS_MAX_FRAME_DATA_LENGTH) break;
+            L = (uint32_t)x;
+        } else {
+            L = plen;
+        }
+        const uint64_t e = p + 2 + ext + (mask ? 4 : 0) + L;
+        if (e > hi) break;
+        p = done = e;
+        if ((b0 & 0x0F) == KMWS_OP_CLOSE) break;
+    }
+    n_out[s] = n;
+    if (consumed) consumed[s] = done - lo;
+}
+
 // ------------------------------ host launchers ------------------------------
 struct CopyWs {
     WsHead* head;
@@ -1273,6 +1335,18 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
     if (n == 0) return KMWS_OK;
     hipLaunchKernelGGL(pack_headers_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, flags, n,
                        reinterpret_cast<u32x4*>(hdr), hl_out);
+    return hip_status(hipGetLastError());
+}
+
+kmws_status kmws_find_headers_streams(const uint8_t* wire, uint64_t wire_len, const uint64_t* stream_off,
+                                      uint32_t n_streams, uint64_t* hdr_off, uint32_t cap, uint32_t* n_out,
+                                      uint64_t* consumed, void* stream)
+{
+    if (n_streams && (!stream_off || !n_out || (cap && !hdr_off) || (wire_len && !wire))) return KMWS_ERR_INVALID_PARAM;
+    if (n_streams == 0) return KMWS_OK;
+    hipLaunchKernelGGL(walk_headers_kernel, dim3((n_streams + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), wire, wire_len, stream_off, n_streams, hdr_off, cap, n_out,
+                       consumed);
     return hip_status(hipGetLastError());
 }
 

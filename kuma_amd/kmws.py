@@ -34,7 +34,7 @@ EXPORTS = [
     "kmws_unmask_batch_variant", "kmws_unmask_autotune", "kmws_unmask_schedule", "kmws_unmask_resident_blocks", "kmws_read_status", "kmws_fill_synthetic",
     "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
-    "kmws_pack_headers_workspace_size", "kmws_pack_headers",
+    "kmws_pack_headers_workspace_size", "kmws_pack_headers", "kmws_find_headers_streams",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
         "kmws_unpack_workspace_size": (sz, []),
         "kmws_pack_headers_workspace_size": (sz, [u32]),
         "kmws_pack_headers": (i32, [vp, vp, u32, u8p, vp, vp, vp, sz, vp]),
+        "kmws_find_headers_streams": (i32, [u8p, u64, vp, u32, vp, u32, vp, vp, vp]),
         "kmws_unpack_headers": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, vp]),
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
@@ -553,6 +554,23 @@ def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Wo
                                    wire_off.data_ptr() if wire_off is not None else None,
                                    ws.ptr if ws is not None else None, ws.nbytes if ws is not None else 0,
                                    _stream_handle(stream)), "kmws_pack_headers")
+
+
+def find_headers_streams(wire, stream_off, cap: int, wire_len: Optional[int] = None, stream=None):
+    """kmws_find_headers_streams: the header-chain walk of every stream
+    wire[stream_off[s]:stream_off[s+1]] on the device, one lane per stream.
+    Returns (hdr_off (n_streams, cap) int64 absolute offsets, n_out int32,
+    consumed int64) device tensors."""
+    import torch
+    ns = stream_off.shape[0] - 1
+    wire_len = wire.numel() if wire_len is None else wire_len
+    hdr = torch.empty((ns, max(cap, 1)), dtype=torch.int64, device=wire.device)
+    n_out = torch.empty(ns, dtype=torch.int32, device=wire.device)
+    consumed = torch.empty(ns, dtype=torch.int64, device=wire.device)
+    _check(lib().kmws_find_headers_streams(wire.data_ptr(), wire_len, stream_off.data_ptr(), ns, hdr.data_ptr(), cap,
+                                           n_out.data_ptr(), consumed.data_ptr(), _stream_handle(stream)),
+           "kmws_find_headers_streams")
+    return hdr, n_out, consumed
 
 
 def unpack_headers(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: Workspace,

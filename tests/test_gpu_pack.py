@@ -280,6 +280,65 @@ def test_pack_headers_parity(T, kind):
     assert T.equal(hdr2, hdr)
 
 
+def test_find_headers_streams_matches_host_walk(T):
+    """kmws_find_headers_streams (one lane per stream) == kmws_find_headers on
+    each stream: complete streams, streams cut mid-frame, a corrupted length,
+    a CLOSE in the middle, empty and 1-byte streams, a cap smaller than the
+    frame count; then the complete streams' offsets feed kmws_unpack_headers."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(zlib.crc32(b"walk-streams"))
+    streams = []
+    for s in range(300):
+        kind = ["mixed", "zipf", "frag4k", "tiny"][s % 4]
+        wire, wire_off, *_ = wire_and_offsets(rng, kind, int(rng.integers(1, 40)))
+        wire = bytearray(wire)
+        cut = s % 7
+        if cut == 1 and len(wire) > 3:    # truncated mid-frame
+            wire = wire[:int(rng.integers(1, len(wire)))]
+        elif cut == 2 and len(wire_off) > 2:  # a 127-class length with bit 63 set
+            wire[int(wire_off[1]) + 1] = (wire[int(wire_off[1]) + 1] & 0x80) | 127
+            wire[int(wire_off[1]) + 2:int(wire_off[1]) + 3] = b"\x80"
+        elif cut == 3:
+            wire = wire[:s % 2]           # empty or one byte
+        elif cut == 4 and len(wire_off) > 2:  # a CLOSE in the middle: the walk stops after it
+            wire[int(wire_off[1])] = (wire[int(wire_off[1])] & 0xF0) | 8
+        streams.append(bytes(wire))
+    cap = 25
+    buf = b"".join(streams)
+    offs = np.concatenate([[0], np.cumsum([len(x) for x in streams])]).astype(np.int64)
+    d_wire = to_dev(T, np.frombuffer(buf, np.uint8).copy() if buf else np.zeros(1, np.uint8))
+    d_off = T.from_numpy(offs).cuda()
+    hdr, n_out, consumed = kmws.find_headers_streams(d_wire, d_off, cap, wire_len=len(buf))
+    T.cuda.synchronize()
+    hdr, n_out, consumed = hdr.cpu().numpy(), n_out.cpu().numpy(), consumed.cpu().numpy()
+    for s, w in enumerate(streams):
+        h, used = kmws.find_headers(w, cap)
+        assert int(n_out[s]) == len(h), s
+        assert [int(x) - int(offs[s]) for x in hdr[s, :len(h)]] == h, s
+        assert int(consumed[s]) == used, s
+    # complete streams back to back: their offsets are one unpackable header list
+    whole = [s for s, w in enumerate(streams) if int(consumed[s]) == len(w) and len(w) and int(n_out[s]) < cap]
+    hl = np.concatenate([hdr[s, :int(n_out[s])] for s in whole])
+    ends = {int(offs[s]) + len(streams[s]) for s in whole}
+    d_hl = T.from_numpy(hl.astype(np.int64)).cuda()
+    od = T.zeros((len(hl), 2), dtype=T.int64, device="cuda")
+    oe = T.full((len(hl),), 99, dtype=T.uint8, device="cuda")
+    ws = kmws.Workspace(kmws.lib().kmws_unpack_workspace_size())
+    kmws.unpack_headers(d_wire, d_hl, kmws.SERVER, od, None, oe, ws, wire_len=len(buf))
+    T.cuda.synchronize()
+    dd = od.cpu().numpy().view(orc.DESC_DTYPE).reshape(-1)
+    assert (oe.cpu().numpy() == 0).all()
+    i = 0
+    for s_ in whole:  # the oracle decoding each whole stream gives the same frames
+        rets, fr = orc.decode_chunks(streams[s_], orc.SERVER, 0)
+        assert rets == [0] and len(fr) == int(n_out[s_]), s_
+        for f in fr:
+            assert int(dd["len"][i]) == f.length and int(dd["key"][i]) == int.from_bytes(f.maskey, "little"), (s_, i)
+            i += 1
+    assert i == len(hl)
+    assert ends  # some complete streams were checked
+
+
 @pytest.mark.parametrize("chunks", [3, 8])
 def test_pack_chunks_knob(T, chunks):
     """The chunked pack pipeline (KMWS_PACK_CHUNKS, read once per process) in a

@@ -371,6 +371,15 @@ def cfg4(reps: int, messages: int):
     w = wire[:P + H].view(n, L + 8)[:, 8:]
     verified = bool(torch.equal(w.reshape(-1), src[:P]))
     t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), reps)
+    # device boundary discovery: the wire cut into S streams at message boundaries, one lane per stream
+    walk = {}
+    for S in (4096, 65536):
+        per = n // S
+        soff = torch.cat([wire_off[0:n:per], wire_off[n:n + 1]]).contiguous()
+        hdr_w, n_w, _ = kmws.find_headers_streams(wire, soff, per, wire_len=P + H)
+        t_w = timed(torch, lambda: kmws.find_headers_streams(wire, soff, per, wire_len=P + H), reps)
+        assert int(n_w.sum()) == n and torch.equal(hdr_w.reshape(-1), wire_off[:n])
+        walk[str(S)] = {"frames_per_stream": per, "ms": t_w * 1e3, "Mheaders_s": n / t_w / 1e6}
     # host boundary discovery rate (the serial part a receiver runs as bytes arrive), 1 GiB sample
     sample = wire[:min(P + H, 1 << 30)].cpu().numpy()
     out = np.zeros(sample.nbytes // 2 + 1, dtype=np.uint64)
@@ -390,6 +399,7 @@ def cfg4(reps: int, messages: int):
             "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30,
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
+            "device_header_walk_by_streams": walk,
             "verified": verified}
 
 
