@@ -906,6 +906,19 @@ __device__ __forceinline__ uint32_t byte_of(const u32x4& v, uint32_t k)
     return (w >> (8u * (k & 3u))) & 0xFFu;
 }
 
+// The 127-class extended length as the reference computes it on x86-64
+// (WSHandler.cpp:176-197): xpl64 |= data[pos] << ((8-k-1) << 3) with a 32-bit
+// int operand, so byte k (0..7) contributes (u64)(i64)(i32)(b << ((7-k)*8 & 31))
+// -- bytes 0..3 alias onto bits 24/16/8/0, bytes 0 and 4 sign-extend.
+// hw holds the header from byte 0; the length bytes are 2..9.
+__device__ __forceinline__ uint64_t ext_len127(const u32x4& hw)
+{
+    uint64_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << (((7u - k) * 8u) & 31u));
+    return x;
+}
+
 // One lane per frame: the reference's HDR1..MASKEY rules (WSHandler.cpp:118-234).
 // The (at most 14) header bytes come from ONE pair of aligned 16-byte loads,
 // funnel-shifted into a register word, when both words lie inside the wire;
@@ -965,12 +978,7 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
                 len = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
                 if (len < 126) err = KMWS_WS_INVALID_LENGTH;
             } else if (plen == 127) {                          // :176-197, x86-64 shift quirk
-                uint64_t x = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < 8; ++k) {
-                    const uint32_t sh = ((7u - k) * 8u) & 31u;
-                    x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << sh);
-                }
+                const uint64_t x = ext_len127(hw);
                 if ((x >> 63) != 0) err = KMWS_WS_INVALID_LENGTH;
                 else {
                     len = (uint32_t)x;
@@ -1073,10 +1081,7 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
         if (plen == 126) {
             L = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
         } else if (plen == 127) {
-            uint64_t x = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k)
-                x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << (((7u - k) * 8u) & 31u));
+            const uint64_t x = ext_len127(hw);
             if ((x >> 63) != 0 || (uint32_t)x > KMWS_MAX_FRAME_DATA_LENGTH) break;
             L = (uint32_t)x;
         } else {

@@ -157,3 +157,21 @@ def test_tx_batch_without_device_is_null():
     assert not kmws.lib().kmws_tx_batch_create(0)
     with pytest.raises(RuntimeError):
         kmws.TxBatch()
+
+
+def test_batch_entries_reject_bad_arguments_before_any_device_work():
+    """Argument checks of the device batch entries return kuma's INVALID_PARAM /
+    BUFFER_TOO_SMALL without launching anything (so they hold with no GPU)."""
+    import ctypes as C
+    L = kmws.lib()
+    fake = C.c_void_p(16)      # never dereferenced: every call below fails its checks first
+    odd = C.c_void_p(16 + 8)   # not 16-byte aligned
+    assert L.kmws_pack_headers(None, None, 5, fake, None, None, None, 0, None) == kmws.ERR_INVALID_PARAM
+    assert L.kmws_pack_headers(fake, fake, 5, odd, None, None, None, 0, None) == kmws.ERR_INVALID_PARAM
+    assert L.kmws_pack_headers(fake, fake, 5, fake, None, fake, None, 0, None) == kmws.ERR_INVALID_PARAM
+    need = L.kmws_pack_headers_workspace_size(5)
+    assert need >= 16
+    assert L.kmws_pack_headers(fake, fake, 5, fake, None, fake, fake, need - 1, None) == kmws.ERR_BUFFER_TOO_SMALL
+    assert L.kmws_find_headers_streams(fake, 64, None, 3, fake, 4, fake, None, None) == kmws.ERR_INVALID_PARAM
+    assert L.kmws_find_headers_streams(fake, 64, fake, 3, None, 4, fake, None, None) == kmws.ERR_INVALID_PARAM
+    assert L.kmws_find_headers_streams(None, 0, None, 0, None, 0, None, None, None) == 0  # nothing to do
