@@ -324,7 +324,8 @@ kmws_status kmws_find_headers(const uint8_t* wire, uint64_t len, uint64_t* hdr_o
  * stream -- frame k+1 starts where frame k's header says -- so a batch gets its
  * parallelism from connections; SURVEY 8 "hard parts").  Stream s is
  * wire[stream_off[s] .. stream_off[s+1]) (stream_off: n_streams+1 ascending
- * entries, stream_off[n_streams] <= wire_len).  Its header offsets (absolute,
+ * entries, stream_off[n_streams] <= wire_len; a stream reaching past wire_len
+ * is cut there).  Its header offsets (absolute,
  * into wire) go to hdr_off[s * cap .. s * cap + n_out[s]); consumed[s] (may be
  * NULL) = bytes of stream s covered by its complete frames.  Stopping rules as
  * kmws_find_headers: cap frames, a truncated frame or invalid length (recorded),

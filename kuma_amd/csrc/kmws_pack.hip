@@ -1051,7 +1051,9 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 {
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= n_streams) return;
-    const uint64_t lo = stream_off[s], hi = stream_off[s + 1];
+    // a stream is clamped to the wire (bad offsets walk nothing instead of reading past it)
+    const uint64_t hi = stream_off[s + 1] < wire_len ? stream_off[s + 1] : wire_len;
+    const uint64_t lo = stream_off[s] < hi ? stream_off[s] : hi;
     const uintptr_t end16 = (reinterpret_cast<uintptr_t>(wire) + wire_len + 15) & ~(uintptr_t)15;
     uint64_t* out = hdr_off + (uint64_t)s * cap;
     uint64_t p = lo, done = lo;
