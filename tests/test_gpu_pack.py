@@ -316,6 +316,12 @@ def test_find_headers_streams_matches_host_walk(T):
         assert int(n_out[s]) == len(h), s
         assert [int(x) - int(offs[s]) for x in hdr[s, :len(h)]] == h, s
         assert int(consumed[s]) == used, s
+    # offsets past the wire are cut at its end (no read beyond it)
+    bad = offs.copy()
+    bad[-1] = len(buf) + 4096
+    hb, nb, cb = kmws.find_headers_streams(d_wire, T.from_numpy(bad).cuda(), cap, wire_len=len(buf))
+    T.cuda.synchronize()
+    assert T.equal(nb.cpu(), T.from_numpy(n_out)) and T.equal(cb.cpu(), T.from_numpy(consumed))
     # complete streams back to back: their offsets are one unpackable header list
     whole = [s for s, w in enumerate(streams) if int(consumed[s]) == len(w) and len(w) and int(n_out[s]) < cap]
     hl = np.concatenate([hdr[s, :int(n_out[s])] for s in whole])
