@@ -136,6 +136,27 @@ def test_fuzz_encode_unpack_gather(T):
         assert int(out_err.max()) == 0 and ws_u.status() == 0 and ws_g.status() == 0
         orig = b"".join(bytes(src[int(o):int(o) + int(L)]) for o, L in zip(offs, lens))
         assert bytes(dst.cpu().numpy()[:len(orig)]) == orig, "gathered payloads differ"
+        # header-only pack: each 16-B slot is the wire image's header, zero-padded
+        hdr = T.zeros(16 * n, dtype=T.uint8, device="cuda")
+        hl = T.zeros(n, dtype=T.uint8, device="cuda")
+        kmws.pack_headers(descs, fl, hdr, hl)
+        # device header-chain walk of the wire cut into random streams at frame boundaries
+        cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n + 1, size=int(rng.integers(0, 8)))]))
+        woff = np.concatenate([want_off, [total]]).astype(np.int64)
+        soff = T.from_numpy(woff[cuts]).cuda()
+        h_w, n_w, c_w = kmws.find_headers_streams(wire, soff, n, wire_len=total)
+        T.cuda.synchronize()
+        H, HL = hdr.cpu().numpy().reshape(n, 16), hl.cpu().numpy()
+        for i in range(n):
+            a = int(want_off[i])
+            b = int(want_off[i + 1]) if i + 1 < n else total
+            assert bytes(H[i, :int(HL[i])]) == bytes(want[a:a + int(HL[i])]) and not H[i, int(HL[i]):].any(), i
+            assert int(HL[i]) + int(lens[i]) == b - a, i
+        h_w, n_w, c_w = h_w.cpu().numpy(), n_w.cpu().numpy(), c_w.cpu().numpy()
+        for j in range(len(cuts) - 1):
+            lo, hi = int(cuts[j]), int(cuts[j + 1])
+            assert int(n_w[j]) == hi - lo and int(c_w[j]) == int(woff[hi] - woff[lo]), j
+            assert np.array_equal(h_w[j, :hi - lo], woff[lo:hi]), j
 
     print("encode/unpack/gather cases:", budget_loop(case))
 
