@@ -19,6 +19,10 @@
 // (WSHandler.cpp:118-234, including the 127-length quirk); the payload is then
 // unmasked in place (kmws_unmask_batch) or gathered + unmasked into a dense
 // arena by the same copy kernels (kmws_gather_unmask).
+// Header-only pack (kmws_pack_headers, kuma's iovec form): the scan's emit
+// pass writes each header into a 16-byte slot.  Boundary discovery on the
+// device (kmws_find_headers_streams): the serial header-chain walk, one lane
+// per stream.
 #include "kmws_common.hpp"
 
 namespace kmws {
