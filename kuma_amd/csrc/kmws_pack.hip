@@ -1047,6 +1047,46 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
 // step reads the (at most 10) bytes it needs from one pair of aligned 16-byte
 // loads (byte loads near the wire's end), decodes the length class (with the
 // 127-class shift quirk) and jumps over the payload.
+// One step of the walk at p (already recorded): false = stop after this frame
+// (truncated, invalid length, CLOSE); else p = done = the next header.
+__device__ __forceinline__ bool walk_step(const uint8_t* __restrict__ wire, uintptr_t end16, uint64_t hi, uint64_t& p,
+                                          uint64_t& done)
+{
+    if (p + 2 > hi) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(wire + p), a16 = a & ~(uintptr_t)15;
+    u32x4 hw = u32x4{0, 0, 0, 0};
+    if (a16 + 32 <= end16) {
+        hw = funnel16(*reinterpret_cast<const u32x4*>(a16), *reinterpret_cast<const u32x4*>(a16 + 16),
+                      (uint32_t)(a & 15u));
+    } else {
+        const uint64_t avail = hi - p < 10 ? hi - p : 10;
+        for (uint32_t k = 0; k < (uint32_t)avail; ++k) {
+            const uint32_t b = wire[p + k], sh = 8u * (k & 3u);
+            if ((k >> 2) == 0) hw.x |= b << sh;
+            else if ((k >> 2) == 1) hw.y |= b << sh;
+            else hw.z |= b << sh;
+        }
+    }
+    const uint32_t b0 = hw.x & 0xFFu, b1 = (hw.x >> 8) & 0xFFu;
+    const uint32_t plen = b1 & 0x7F, mask = b1 >> 7;
+    const uint64_t ext = plen == 126 ? 2 : (plen == 127 ? 8 : 0);
+    if (p + 2 + ext > hi) return false;
+    uint64_t L;
+    if (plen == 126) {
+        L = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
+    } else if (plen == 127) {
+        const uint64_t x = ext_len127(hw);
+        if ((x >> 63) != 0 || (uint32_t)x > KMWS_MAX_FRAME_DATA_LENGTH) return false;
+        L = (uint32_t)x;
+    } else {
+        L = plen;
+    }
+    const uint64_t e = p + 2 + ext + (mask ? 4 : 0) + L;
+    if (e > hi) return false;
+    p = done = e;
+    return (b0 & 0x0F) != KMWS_OP_CLOSE;
+}
+
 __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                               const uint64_t* __restrict__ stream_off,
                                                               uint32_t n_streams, uint64_t* __restrict__ hdr_off,
@@ -1062,41 +1102,29 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
     uint64_t* out = hdr_off + (uint64_t)s * cap;
     uint64_t p = lo, done = lo;
     uint32_t n = 0;
-    while (p < hi && n < cap) {
-        out[n++] = p;
-        if (p + 2 > hi) break;
-        const uintptr_t a = reinterpret_cast<uintptr_t>(wire + p), a16 = a & ~(uintptr_t)15;
-        u32x4 hw = u32x4{0, 0, 0, 0};
-        if (a16 + 32 <= end16) {
-            hw = funnel16(*reinterpret_cast<const u32x4*>(a16), *reinterpret_cast<const u32x4*>(a16 + 16),
-                          (uint32_t)(a & 15u));
-        } else {
-            const uint64_t avail = hi - p < 10 ? hi - p : 10;
-            for (uint32_t k = 0; k < (uint32_t)avail; ++k) {
-                const uint32_t b = wire[p + k], sh = 8u * (k & 3u);
-                if ((k >> 2) == 0) hw.x |= b << sh;
-                else if ((k >> 2) == 1) hw.y |= b << sh;
-                else hw.z |= b << sh;
+    bool stop = false;
+    // Offsets are kept in registers and written 16 at a time (128 bytes, a whole
+    // line per lane): one 8-byte store per lane and step left partial lines of
+    // thousands of streams in flight, and the L2 wrote them back piecewise.
+    while (!stop) {
+        uint64_t buf[16];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (!stop) {
+                if (p >= hi || n >= cap) {
+                    stop = true;
+                } else {
+                    buf[j] = p;
+                    cnt = j + 1;
+                    ++n;
+                    stop = !walk_step(wire, end16, hi, p, done);
+                }
             }
         }
-        const uint32_t b0 = hw.x & 0xFFu, b1 = (hw.x >> 8) & 0xFFu;
-        const uint32_t plen = b1 & 0x7F, mask = b1 >> 7;
-        const uint64_t ext = plen == 126 ? 2 : (plen == 127 ? 8 : 0);
-        if (p + 2 + ext > hi) break;
-        uint64_t L;
-        if (plen == 126) {
-            L = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
-        } else if (plen == 127) {
-            const uint64_t x = ext_len127(hw);
-            if ((x >> 63) != 0 || (uint32_t)x > KMWS_MAX_FRAME_DATA_LENGTH) break;
-            L = (uint32_t)x;
-        } else {
-            L = plen;
-        }
-        const uint64_t e = p + 2 + ext + (mask ? 4 : 0) + L;
-        if (e > hi) break;
-        p = done = e;
-        if ((b0 & 0x0F) == KMWS_OP_CLOSE) break;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if ((uint32_t)j < cnt) out[n - cnt + j] = buf[j];
     }
     n_out[s] = n;
     if (consumed) consumed[s] = done - lo;
