@@ -67,7 +67,7 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint
 }
 
 // Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
-template <int V, bool FULL>
+template <int V, bool FULL, bool TWO = false>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
                                             const kmws_desc* __restrict__ d, uint32_t n,
                                             const uint32_t* __restrict__ map, uint32_t tile, bool ok,
@@ -90,6 +90,42 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
             if (ok) __builtin_nontemporal_store(v[i] ^ r, reinterpret_cast<u32x4*>(base + a));
+        }
+        return;
+    }
+
+    // Two frames at most (a frame boundary inside the tile, e.g. a packed wire
+    // image of frames longer than a tile): both descriptors are block-uniform
+    // scalars, each word's mask is built from them directly -- no LDS, no
+    // barrier (at 2 blocks per CU a barrier's latency is not hidden; TWO: the
+    // capped launches; uncapped, the LDS path measured faster on 4 KiB frames).
+    // Words whose mask is zero (headers, gaps) are not stored.
+    if (TWO && FULL && flast <= f + 1 && f < n) {
+        const kmws_desc d1 = flast > f && flast < n ? d[flast] : kmws_desc{~0ull, 0u, 0u};
+        const uint32_t r0 = rot_key(d0.key, d0.off), r1 = rot_key(d1.key, d1.off);
+        const uint64_t e0 = d0.off + d0.len, e1 = d1.off + d1.len;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
+            u32x4 mm = u32x4{0, 0, 0, 0};
+            if (d0.off <= a && e0 >= a + 16) {
+                mm = u32x4{r0, r0, r0, r0};
+            } else if (d1.off <= a && e1 >= a + 16) {
+                mm = u32x4{r1, r1, r1, r1};
+            } else {  // a word holding a frame edge: byte-exact
+                if (d0.off < a + 16 && e0 > a) {
+                    const int blo = d0.off > a ? (int)(d0.off - a) : 0, bhi = e0 < a + 16 ? (int)(e0 - a) : 16;
+                    mm |= u32x4{r0 & dword_byte_mask(blo, bhi, 0), r0 & dword_byte_mask(blo, bhi, 1),
+                                r0 & dword_byte_mask(blo, bhi, 2), r0 & dword_byte_mask(blo, bhi, 3)};
+                }
+                if (d1.off < a + 16 && e1 > a) {
+                    const int blo = d1.off > a ? (int)(d1.off - a) : 0, bhi = e1 < a + 16 ? (int)(e1 - a) : 16;
+                    mm |= u32x4{r1 & dword_byte_mask(blo, bhi, 0), r1 & dword_byte_mask(blo, bhi, 1),
+                                r1 & dword_byte_mask(blo, bhi, 2), r1 & dword_byte_mask(blo, bhi, 3)};
+                }
+            }
+            if (ok && (mm.x | mm.y | mm.z | mm.w) != 0u)
+                __builtin_nontemporal_store(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a));
         }
         return;
     }
@@ -153,7 +189,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
 
 // One block per tile.  W = minimum waves per SIMD the register allocation must
 // allow (1 = unconstrained; the tuning variants test 6 and 8).
-template <int V, int W = 1>
+template <int V, int W = 1, bool TWO = false>
 __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
@@ -172,7 +208,7 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
     if (tile_lo + Cfg::kTile <= span) {
         load_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off,
+        finish_tile<V, true, TWO>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off,
                              s_end, s_key);
     } else {
         load_tile<V, false>(base, tile_lo, span, v);
@@ -188,7 +224,7 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
 // its own runs).
-template <int V>
+template <int V, bool TWO = false>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
@@ -224,7 +260,7 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     u32x4 v[V];
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
+    finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
 }
 
 // Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
@@ -428,6 +464,47 @@ constexpr int kMaxDevices = 64;
 static uint32_t g_schedule[kMaxDevices];
 using ProdCfg = UnmaskCfg<kUnmaskV>;
 
+// Blocks of an apply grid resident per CU.  Fewer blocks in flight stream HBM
+// better: 2 blocks of 256 lanes per CU (32 KiB of loads in flight per CU) run
+// the 64 GiB batch at 84.5-84.8 % of peak against 82.4-82.9 % with the 6 the
+// registers allow, 3 blocks at 83.4 %, 1 block at 65-75 %
+// (profiles/r02ag_unmask_occupancy.txt).  The cap is dynamic LDS the kernel does
+// not use: a block asks for just over a third of the CU's LDS.
+// KMWS_UNMASK_BLOCKS_PER_CU overrides it (0 = no cap; tuning).
+constexpr uint32_t kUnmaskBlocksPerCU = 2;
+constexpr uint32_t kUnmaskStaticLds = UnmaskCfg<4>::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
+static unsigned unmask_lds_pad_device();
+// The cap pays where tiles take the one- or two-frame paths; batches of small
+// frames (several per tile: the LDS-staged path, whose barriers need the
+// latency hiding of a full CU) keep every block: 4 KiB frames ran at 47.6 % capped
+// vs 80 % uncapped.  Mean region >= 2 tiles selects.
+static unsigned unmask_lds_pad(uint64_t span, uint32_t n)
+{
+    return n && span / n >= 2 * UnmaskCfg<4>::kTile ? unmask_lds_pad_device() : 0u;
+}
+static unsigned unmask_lds_pad_device()
+{
+    static thread_local int dev_cached = -1;
+    static thread_local unsigned pad = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev != dev_cached) {
+        static const int want = [] {
+            const char* e = getenv("KMWS_UNMASK_BLOCKS_PER_CU");
+            return e ? atoi(e) : (int)kUnmaskBlocksPerCU;
+        }();
+        int lds = 0;
+        pad = 0;
+        if (want > 0 && hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) ==
+                            hipSuccess && lds > 0) {
+            const unsigned per_block = (unsigned)lds / (unsigned)(want + 1) + 1;  // want + 1 blocks do not fit
+            pad = per_block > kUnmaskStaticLds ? per_block - kUnmaskStaticLds : 0u;
+        }
+        dev_cached = dev;
+    }
+    return pad;
+}
+
 static uint32_t ilog2_u64(uint64_t x)
 {
     uint32_t r = 0;
@@ -474,8 +551,13 @@ static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* d
     constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
     for (uint64_t t0 = 0; t0 < ntiles; t0 += kMaxBlocks) {
         const uint64_t nb = ntiles - t0 < kMaxBlocks ? ntiles - t0 : kMaxBlocks;
-        hipLaunchKernelGGL((unmask_tiles_kernel<V, W>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs,
-                           n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
+        const unsigned pad = unmask_lds_pad(span, n);
+        if (pad)
+            hipLaunchKernelGGL((unmask_tiles_kernel<V, W, true>), dim3((uint32_t)nb), dim3(kBlock), pad, s, base, span,
+                               descs, n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
+        else
+            hipLaunchKernelGGL((unmask_tiles_kernel<V, W>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs,
+                               n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
     }
     return hip_status(hipGetLastError());
 }
@@ -554,10 +636,15 @@ static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_d
     if (nfull > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
     // a launch may hold at most 2^32 work-items: huge spans go in pieces of blocks
     constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
+    const unsigned lds_pad = unmask_lds_pad(span, n);
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
-        hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
-                           head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+        if (lds_pad)
+            hipLaunchKernelGGL((unmask_split_kernel<V, true>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s, base, descs,
+                               n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+        else
+            hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
+                               head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,

@@ -366,6 +366,7 @@ def cfg4(reps: int, messages: int):
     assert int(out_err.max()) == 0
     assert torch.equal(out_flags.cpu(), fl16.cpu())
     ws_m = kmws.Workspace(kmws.unmask_workspace_size(P + H))
+    sched = kmws.unmask_autotune(wire, out_desc, ws_m, P + H)  # this batch's schedule (payload unchanged)
     kmws.unmask_batch(wire, out_desc, ws_m, P + H)   # once, then verify, then time pairs (identity)
     torch.cuda.synchronize()
     w = wire[:P + H].view(n, L + 8)[:, 8:]
@@ -396,7 +397,7 @@ def cfg4(reps: int, messages: int):
                                   # desc 16 + flags 2 in, slot 16 + length 1 + wire offset 8 out
                                   "hbm_frac": 43 * n / t_hdr / 8e12},
             "unpack": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
-            "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30,
+            "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30, "schedule": sched,
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
             "device_header_walk_by_streams": walk,
