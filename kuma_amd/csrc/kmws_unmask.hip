@@ -720,8 +720,8 @@ extern "C" {
 
 size_t kmws_unmask_workspace_size(uint64_t span)
 {
-    // sized for the smallest tile any variant uses
-    const uint64_t ntiles = (span + UnmaskCfg<4>::kTile - 1) / UnmaskCfg<4>::kTile;
+    // sized for the smallest tile any variant uses (8 KiB: variants 40, 41)
+    const uint64_t ntiles = (span + UnmaskCfg<2>::kTile - 1) / UnmaskCfg<2>::kTile;
     return sizeof(WsHead) + (size_t)(ntiles + 1) * sizeof(uint32_t);  // + the map's sentinel
 }
 
@@ -882,6 +882,13 @@ kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_d
         if (st != KMWS_OK) return st;
         return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, 16u,
                                      2u << (variant - 36));
+    }
+    case 40:
+    case 41: {  // 8 KiB tiles, one block per tile: split 8 / XCD runs of 32 tiles
+        kmws_status st = launch_plan<2>(span, descs, n, workspace, workspace_bytes, s);
+        if (st != KMWS_OK) return st;
+        return variant == 40 ? launch_apply_split<2>(base, span, descs, n, workspace, workspace_bytes, s, 8u)
+                             : launch_apply_split<2>(base, span, descs, n, workspace, workspace_bytes, s, 8u, 32u);
     }
     default:
         if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)
