@@ -470,7 +470,7 @@ using ProdCfg = UnmaskCfg<kUnmaskV>;
 // registers allow, 3 blocks at 83.4 %, 1 block at 65-75 %
 // (profiles/r02ag_unmask_occupancy.txt).  The cap is dynamic LDS the kernel does
 // not use: a block asks for just over a third of the CU's LDS.
-// KMWS_UNMASK_BLOCKS_PER_CU overrides it (0 = no cap; tuning).
+// KMWS_UNMASK_BLOCKS_PER_CU overrides it for every batch (0 = no cap; tuning).
 constexpr uint32_t kUnmaskBlocksPerCU = 2;
 constexpr uint32_t kUnmaskStaticLds = UnmaskCfg<4>::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
 static unsigned unmask_lds_pad_device();
@@ -480,7 +480,8 @@ static unsigned unmask_lds_pad_device();
 // vs 80 % uncapped.  Mean region >= 2 tiles selects.
 static unsigned unmask_lds_pad(uint64_t span, uint32_t n)
 {
-    return n && span / n >= 2 * UnmaskCfg<4>::kTile ? unmask_lds_pad_device() : 0u;
+    static const bool forced = getenv("KMWS_UNMASK_BLOCKS_PER_CU") != nullptr;  // tuning: the cap on every batch
+    return forced || (n && span / n >= 2 * UnmaskCfg<4>::kTile) ? unmask_lds_pad_device() : 0u;
 }
 static unsigned unmask_lds_pad_device()
 {
