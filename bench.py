@@ -105,7 +105,7 @@ def _cpu_model() -> str:
 
 def schedule_kernel(schedule: int) -> str:
     """Kernel that carries the unmask for a kmws_unmask_schedule() code."""
-    if schedule in (0, 2, 3, 4):
+    if schedule in (0, 2, 3, 4, 5):
         return "unmask_split_kernel"
     if schedule == 1:
         return "unmask_tiles_kernel"
@@ -117,8 +117,8 @@ def schedule_name(schedule: int) -> str:
         return "one block per 16 KiB tile, 2 groups of 4 XCDs, runs of 16 tiles per XCD in the group's half"
     if schedule == 4:
         return "one block per 16 KiB tile, runs of 16 tiles per XCD"
-    if schedule in (2, 3):
-        return f"one block per 16 KiB tile, tiles dealt over {8 if schedule == 3 else 2} parts of the span"
+    if schedule in (2, 3, 5):
+        return f"one block per 16 KiB tile, tiles dealt over {dict([(2, 2), (3, 8), (5, 4)])[schedule]} parts of the span"
     if schedule == 1:
         return "one block per 16 KiB tile, in order"
     kind = "pipelined persistent grid" if schedule & 1 else "persistent grid-stride"

@@ -226,7 +226,7 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * current device's schedule for kmws_unmask_apply / kmws_unmask_batch.
  * Returns the chosen schedule or a negative status, one block per 16 KiB tile:
  * the XCDs in 2 groups, each dealing runs of 16 tiles inside its own half of
- * the span (0, the default), in order (1), tiles dealt over 2 (2) or 8 (3)
+ * the span (0, the default), in order (1), tiles dealt over 2 (2), 8 (3) or 4 (5)
  * far-apart parts of the span, runs of 16 tiles per XCD (4); >= 64: a
  * persistent grid of that many blocks (+1: the pipelined grid).  kmws_unmask_schedule() reports the current one. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,

@@ -676,6 +676,7 @@ static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, 
     if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
     if (code == 2) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 2u);
     if (code == 3) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
+    if (code == 5) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 4u);
     if (code < 64) return KMWS_ERR_INVALID_PARAM;
     if (code & 1u) return launch_apply_pipe<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code & ~1u);
     return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code);
@@ -769,10 +770,11 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     hipStream_t s = static_cast<hipStream_t>(stream);
     kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    // grouped XCD runs, 8 parts, XCD runs, 2 parts, in order: which wins depends on
-    // where the batch lies in HBM and on its frame layout
-    // (profiles/r01f_unmask_placement.txt)
-    static const uint32_t cand[] = {0u, 3u, 4u, 2u, 1u};
+    // grouped XCD runs, 4 parts, 8 parts, XCD runs, 2 parts, in order: which wins
+    // depends on where the batch lies in HBM, on its frame layout and on the
+    // blocks in flight (profiles/r01f_unmask_placement.txt; at 2 blocks per CU
+    // 4 parts led with 85.3 %, profiles/r02al_unmask_schedules_2bpc.txt)
+    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {

@@ -199,7 +199,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
     ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
-    assert choice in (0, 1, 2, 3, 4) and kmws.unmask_schedule() == choice
+    assert choice in (0, 1, 2, 3, 4, 5) and kmws.unmask_schedule() == choice
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
@@ -208,7 +208,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
 
 
 @pytest.mark.parametrize("frame_len,tail", [(65536, 0), (65531, 0), (3000, 0), (65531, 7 * 16384 + 100)])
-@pytest.mark.parametrize("variant", [None, 4, 10, 21, 23, 24, 25, 27, 29, 30, 36, 37, 38, 2097152, 65537])
+@pytest.mark.parametrize("variant", [None, 4, 10, 21, 22, 23, 24, 25, 27, 29, 30, 36, 37, 38, 40, 41, 2097152, 65537])
 def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len, tail):
     """512 MiB arena (32 K tiles: many tiles per block of the persistent
     schedules, whole runs and parts of the XCD-run and split mappings), plus a
