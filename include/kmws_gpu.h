@@ -380,11 +380,11 @@ void  kmws_arena_free(void* p, int device);
 void* kmws_host_alloc(size_t bytes, int device);
 void  kmws_host_free(void* p);
 
-/* Placement probe for a long-lived batch region inside an arena: times an
- * in-place split-8 unmask of `span` bytes (uniform 64 KiB probe frames, applied
- * twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step, ...
- * (offset + span <= arena_bytes) and returns the byte offset of the fastest,
- * or a negative kmws_status.  The split schedules run 76 % or 82-83 % of HBM
+/* Placement probe for a long-lived batch region inside an arena: times in-place
+ * split-4 and split-8 unmasks of `span` bytes (uniform 64 KiB probe frames, each
+ * applied twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step,
+ * ... (offset + span <= arena_bytes) and returns the byte offset where the better
+ * of the two is fastest, or a negative kmws_status.  The split schedules run 76 % or 82-85 % of HBM
  * peak depending on where the batch lies in physical HBM, which the kernel
  * cannot see (DESIGN.md sec.4 "Placement").  frac_out (optional, max_out
  * entries) receives each offset's rate as a fraction of 8 TB/s.  A setup call:

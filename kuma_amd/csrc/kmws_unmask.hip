@@ -949,7 +949,9 @@ int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, ui
 {
     // Offsets 0, step, 2 step, ... with offset + span <= arena_bytes.  The probe
     // batch: uniform 64 KiB frames over the span (contents are whatever the arena
-    // holds; XOR applied twice leaves them unchanged), split-8 schedule (code 3).
+    // holds; XOR applied twice leaves them unchanged); an offset scores the better
+    // of the split-4 and split-8 schedules (codes 5, 3: which one leads depends
+    // on the placement, and kmws_unmask_autotune then picks among all).
     constexpr uint64_t kFrame = 65536;
     if (!arena || span == 0 || span > arena_bytes || step == 0 || (step & 15u) ||
         (reinterpret_cast<uintptr_t>(arena) & 15u) || span / kFrame > 0xFFFFFFFFull)
@@ -978,11 +980,11 @@ int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, ui
         uint32_t k = 0;
         for (uint64_t off = 0; st == KMWS_OK && off + span <= arena_bytes; off += step, ++k) {
             float t = 1e30f;
-            for (int rep = 0; rep < 2 && st == KMWS_OK; ++rep) {  // min of two pairs
+            for (int rep = 0; rep < 4 && st == KMWS_OK; ++rep) {  // min of two pairs per schedule
                 st = launch_plan<kUnmaskV>(span, d, n, ws, ws_bytes, s);
                 if (st == KMWS_OK) st = hip_status(hipEventRecord(e0, s));
                 for (int i = 0; i < 2 && st == KMWS_OK; ++i)
-                    st = launch_schedule(3u, arena + off, span, d, n, ws, ws_bytes, s);
+                    st = launch_schedule(rep & 1 ? 3u : 5u, arena + off, span, d, n, ws, ws_bytes, s);
                 if (st == KMWS_OK) st = hip_status(hipEventRecord(e1, s));
                 if (st == KMWS_OK) st = hip_status(hipEventSynchronize(e1));
                 float ms = 0;
