@@ -18,6 +18,9 @@ python3 tools/pmc_traffic.py "$OUT/split_fetch" "$OUT/split_write" unmask_split_
 pass split8_fetch FETCH_SIZE "--variant 23" &&
 pass split8_write WRITE_SIZE "--variant 23" &&
 python3 tools/pmc_traffic.py "$OUT/split8_fetch" "$OUT/split8_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split8.json" 3 &&
+pass split4_fetch FETCH_SIZE "--variant 22" &&
+pass split4_write WRITE_SIZE "--variant 22" &&
+python3 tools/pmc_traffic.py "$OUT/split4_fetch" "$OUT/split4_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_split4.json" 5 &&
 pass runs_fetch FETCH_SIZE "--variant 27" &&
 pass runs_write WRITE_SIZE "--variant 27" &&
 python3 tools/pmc_traffic.py "$OUT/runs_fetch" "$OUT/runs_write" unmask_split_kernel 1048576 65536 "$OUT/traffic_runs.json" 4 &&
