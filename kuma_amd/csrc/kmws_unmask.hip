@@ -474,14 +474,16 @@ using ProdCfg = UnmaskCfg<kUnmaskV>;
 constexpr uint32_t kUnmaskBlocksPerCU = 2;
 constexpr uint32_t kUnmaskStaticLds = UnmaskCfg<4>::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
 static unsigned unmask_lds_pad_device();
-// The cap pays where tiles take the one- or two-frame paths; batches of small
-// frames (several per tile: the LDS-staged path, whose barriers need the
-// latency hiding of a full CU) keep every block: 4 KiB frames ran at 47.6 % capped
-// vs 80 % uncapped.  Mean region >= 2 tiles selects.
+// The cap pays where tiles take the one- or two-frame paths (regions of a tile
+// or more: 16 KiB frames ran 85.5 % capped vs 79-83 % uncapped); batches of
+// smaller frames (several per tile: the LDS-staged path, whose barriers need the
+// latency hiding of a full CU) keep every block: 8 KiB frames ran 54.8 % capped
+// vs 83 %, 4 KiB frames 47.6 % vs 80 % (profiles/r02at_unmask_framelen_occupancy.txt).
+// Mean region >= 1 tile selects.
 static unsigned unmask_lds_pad(uint64_t span, uint32_t n)
 {
     static const bool forced = getenv("KMWS_UNMASK_BLOCKS_PER_CU") != nullptr;  // tuning: the cap on every batch
-    return forced || (n && span / n >= 2 * UnmaskCfg<4>::kTile) ? unmask_lds_pad_device() : 0u;
+    return forced || (n && span / n >= UnmaskCfg<4>::kTile) ? unmask_lds_pad_device() : 0u;
 }
 static unsigned unmask_lds_pad_device()
 {
