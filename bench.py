@@ -363,7 +363,7 @@ def place_batch(kmws, torch, dev, span, slack):
         return None, None, {"kind": "plain torch.empty", "why": str(e)}
     off, probe = kmws.arena_place(arena, span, PLACEMENT_STEP)  # kmws_arena_place: timed split-8 passes
     pick = off >> 30
-    rec = {"kind": "offset in a contiguous arena, picked by kmws_arena_place (timed split-8 probe)",
+    rec = {"kind": "offset in a contiguous arena, picked by kmws_arena_place (timed probe: best of split 4 and split 8 per offset)",
            "arena_GiB": (span + slack) >> 30, "contiguous": arena.contiguous, "offset_GiB": pick,
            "probe_frac_by_offset_GiB": {o >> 30: v for o, v in probe.items()}}
     return arena, arena.tensor[pick << 30:(pick << 30) + span], rec
