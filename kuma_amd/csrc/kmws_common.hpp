@@ -12,8 +12,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
 
-// First 16 bytes of every workspace: status word (+ pad), zeroed by a
-// hipMemsetAsync at the start of each batch call.
+// First 16 bytes of every workspace: status word (+ pad), zeroed by
+// launch_zero (a kernel, not a memset node: see below) at the start of each
+// batch call.
 struct WsHead {
     uint32_t status;
     uint32_t pad[3];

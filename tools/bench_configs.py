@@ -77,6 +77,19 @@ def verify_dense(torch, src, src_off, lens, dst, dst_off, frames_per_chunk=20000
     return True
 
 
+def placed_buffer(torch, kmws, span: int):
+    """A device buffer of `span` bytes carved from a contiguous arena at the
+    offset where the placement probe runs fastest (bench.place_batch, the
+    headline bench's placement; DESIGN.md sec.4 'Placement of the batch').
+    Returns (arena or None, uint8 view, placement record)."""
+    import bench
+    dev = torch.device("cuda", torch.cuda.current_device())
+    arena, view, rec = bench.place_batch(kmws, torch, dev, span, 96 << 30)
+    if arena is None:
+        view = torch.empty(span, dtype=torch.uint8, device=dev)
+    return arena, view, rec
+
+
 def timed(torch, fn, reps):
     ts = []
     for _ in range(reps):
@@ -298,7 +311,7 @@ def _cfg3_e2e_run(torch, kmws, host_src, host_dst, P, n, lens, pay_off, rel, fla
                     "3 slots on 3 streams; PCIe-bound (each payload byte crosses twice)"}
 
 
-def cfg2b(reps: int, frames: int):
+def cfg2b(reps: int, frames: int, placed: bool = True):
     """BASELINE configs[1] variant B (SURVEY 8 d row 2): the same 1 M x 64 KiB
     frames as a packed wire image -- 14-byte masked headers between payloads,
     so payload starts are misaligned (payload f at 14 + f * 65,550) -- unmasked
@@ -316,19 +329,36 @@ def cfg2b(reps: int, frames: int):
     kmws.fill_uniform_descs(descs, L + H, L, SEED ^ 7)
     descs[:, 0] += H
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
-    sched = kmws.unmask_autotune(wire, descs, ws, span)
-    kmws.unmask_batch(wire, descs, ws, span)  # odd number of passes in total: verify the masked state
-    t = timed(torch, lambda: kmws.unmask_batch(wire, descs, ws, span), 2 * (reps // 2) + 2)  # even: back to masked
-    ok = ws.status() == 0 and kmws.check_unmasked(wire, SEED, descs) == 0
     alg = n * (2 * L + 16)
-    return {"config": "cfg2b", "frames": n, "frame_len": L, "header_len": H, "span_bytes": span,
-            "schedule": sched, "ms": t * 1e3, "payload_GiB_s": n * L / t / 2**30,
-            "alg_GB_s": alg / t / 1e9, "hbm_frac": alg / t / 8e12, "verified": bool(ok),
-            "note": "device-resident packed wire (14-B headers, misaligned payloads), in-place unmask, plan + apply"}
+
+    def run(buf):
+        sched = kmws.unmask_autotune(buf, descs, ws, span)
+        kmws.unmask_batch(buf, descs, ws, span)  # odd number of passes in total: verify the masked state
+        t = timed(torch, lambda: kmws.unmask_batch(buf, descs, ws, span), 2 * (reps // 2) + 2)  # even: back to masked
+        ok = ws.status() == 0 and kmws.check_unmasked(buf, SEED, descs) == 0
+        return sched, t, bool(ok)
+
+    sched, t, ok = run(wire)
+    res = {"config": "cfg2b", "frames": n, "frame_len": L, "header_len": H, "span_bytes": span,
+           "schedule": sched, "ms": t * 1e3, "payload_GiB_s": n * L / t / 2**30,
+           "alg_GB_s": alg / t / 1e9, "hbm_frac": alg / t / 8e12, "verified": ok,
+           "note": "device-resident packed wire (14-B headers, misaligned payloads), in-place unmask, plan + apply; "
+                   "top level: plain torch.empty wire; 'placed': the same wire in a probed arena like bench.py"}
+    if placed:
+        del wire
+        torch.cuda.empty_cache()
+        arena, buf, rec = placed_buffer(torch, kmws, span)
+        kmws.fill_synthetic(buf, SEED)
+        sched, t, ok = run(buf)
+        res["placed"] = {"schedule": sched, "ms": t * 1e3, "payload_GiB_s": n * L / t / 2**30,
+                         "hbm_frac": alg / t / 8e12, "verified": ok, "placement": rec}
+        del buf, arena
+        res["verified"] = res["verified"] and ok
+    return res
 
 
 # ------------------------------------------------------------------ cfg4
-def cfg4(reps: int, messages: int):
+def cfg4(reps: int, messages: int, placed: bool = True):
     import torch
     from kuma_amd import kmws
     n, L = messages * 16, 4096
@@ -372,6 +402,18 @@ def cfg4(reps: int, messages: int):
     w = wire[:P + H].view(n, L + 8)[:, 8:]
     verified = bool(torch.equal(w.reshape(-1), src[:P]))
     t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), reps)
+    placed_rec = None
+    if placed:  # the same in-place unmask on a copy of the wire in a placement-probed arena (as bench.py)
+        arena, pw, rec = placed_buffer(torch, kmws, P + H)
+        pw.copy_(wire[:P + H])
+        sched_p = kmws.unmask_autotune(pw, out_desc, ws_m, P + H)
+        t_p = timed(torch, lambda: kmws.unmask_batch(pw, out_desc, ws_m, P + H), 2 * (reps // 2) + 1)  # odd
+        torch.cuda.synchronize()
+        ok_p = ws_m.status() == 0 and bool(torch.equal(pw.view(n, L + 8)[:, 8:].reshape(-1), src[:P]))
+        placed_rec = {"ms": t_p * 1e3, "payload_GiB_s": P / t_p / 2**30, "schedule": sched_p,
+                      "hbm_frac": (2 * P + 16 * n) / t_p / 8e12, "verified": ok_p, "placement": rec}
+        verified = verified and ok_p
+        del pw, arena
     # device boundary discovery: the wire cut into S streams at message boundaries, one lane per stream
     walk = {}
     for S in (4096, 65536):
@@ -398,7 +440,7 @@ def cfg4(reps: int, messages: int):
                                   "hbm_frac": 43 * n / t_hdr / 8e12},
             "unpack": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
             "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30, "schedule": sched,
-                                "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
+                                "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12, "placed": placed_rec},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
             "device_header_walk_by_streams": walk,
             "verified": verified}
@@ -450,6 +492,8 @@ def main():
     ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
     ap.add_argument("--cfg2b-frames", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--placement", default="probe", choices=["probe", "plain"],
+                    help="probe: cfg2b and cfg4's in-place unmask also run in a placement-probed arena, as bench.py")
     ap.add_argument("--cfg3-gib", type=float, default=8.0)
     ap.add_argument("--cfg4-messages", type=int, default=262144)
     ap.add_argument("--e2e-gib", type=float, default=8.0)
@@ -460,13 +504,13 @@ def main():
         if w == "cfg1":
             r = cfg1(max(a.reps, 10))
         elif w == "cfg2b":
-            r = cfg2b(a.reps, a.cfg2b_frames)
+            r = cfg2b(a.reps, a.cfg2b_frames, a.placement == "probe")
         elif w == "cfg3":
             r = cfg3(a.reps, a.cfg3_gib)
         elif w == "cfg3_e2e":
             r = cfg3_e2e(a.cfg3_gib, a.e2e_chunk_mib, min(a.reps, 3))
         elif w == "cfg4":
-            r = cfg4(a.reps, a.cfg4_messages)
+            r = cfg4(a.reps, a.cfg4_messages, a.placement == "probe")
         else:
             r = e2e(a.e2e_gib, a.e2e_chunk_mib, a.e2e_depth)
         print(json.dumps(r), flush=True)

@@ -29,7 +29,9 @@ b=json.load(open('$OUT/${b}_bench_$rep.json'))
 c=[json.loads(l) for l in open('$OUT/${b}_cfg_$rep.jsonl')]
 print('rep $rep $b', 'cfg2 %.4f (%s)' % (b['roofline']['frac'], b['config']['unmask_schedule'][:40]),
       'cfg2b %.4f (sched %s)' % (c[0]['hbm_frac'], c[0]['schedule']),
-      'cfg4 unmask %.4f (sched %s)' % (c[1]['unmask_in_place']['hbm_frac'], c[1]['unmask_in_place'].get('schedule')))
+      'placed %.4f (sched %s)' % (c[0].get('placed', {}).get('hbm_frac', 0), c[0].get('placed', {}).get('schedule')),
+      'cfg4 unmask %.4f (sched %s)' % (c[1]['unmask_in_place']['hbm_frac'], c[1]['unmask_in_place'].get('schedule')),
+      'placed %.4f' % ((c[1]['unmask_in_place'].get('placed') or {}).get('hbm_frac', 0)))
 "
   done
 done
