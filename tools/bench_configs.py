@@ -311,7 +311,7 @@ def _cfg3_e2e_run(torch, kmws, host_src, host_dst, P, n, lens, pay_off, rel, fla
                     "3 slots on 3 streams; PCIe-bound (each payload byte crosses twice)"}
 
 
-def cfg2b(reps: int, frames: int, placed: bool = True):
+def cfg2b(reps: int, frames: int, placed: bool = True, header: int = 14):
     """BASELINE configs[1] variant B (SURVEY 8 d row 2): the same 1 M x 64 KiB
     frames as a packed wire image -- 14-byte masked headers between payloads,
     so payload starts are misaligned (payload f at 14 + f * 65,550) -- unmasked
@@ -319,7 +319,7 @@ def cfg2b(reps: int, frames: int, placed: bool = True):
     (descriptor-staged, byte-exact) path; headers keep their bytes."""
     import torch
     from kuma_amd import kmws
-    L, H = 65536, 14
+    L, H = 65536, header
     n = frames
     span = n * (L + H)
     dev = torch.device("cuda")
@@ -491,6 +491,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
     ap.add_argument("--cfg2b-frames", type=int, default=1 << 20)
+    ap.add_argument("--cfg2b-header", type=int, default=14, help="bytes between payloads (14 = masked 64 KiB header)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--placement", default="probe", choices=["probe", "plain"],
                     help="probe: cfg2b and cfg4's in-place unmask also run in a placement-probed arena, as bench.py")
@@ -504,7 +505,7 @@ def main():
         if w == "cfg1":
             r = cfg1(max(a.reps, 10))
         elif w == "cfg2b":
-            r = cfg2b(a.reps, a.cfg2b_frames, a.placement == "probe")
+            r = cfg2b(a.reps, a.cfg2b_frames, a.placement == "probe", a.cfg2b_header)
         elif w == "cfg3":
             r = cfg3(a.reps, a.cfg3_gib)
         elif w == "cfg3_e2e":
