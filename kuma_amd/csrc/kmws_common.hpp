@@ -50,6 +50,21 @@ __device__ __forceinline__ uint32_t dword_byte_mask(int lo, int hi, int d)
     return hm & ~lm;
 }
 
+// Bytes [lo, hi) of a 16-byte word as a lane mask, 0 <= lo, hi <= 16 (empty when
+// hi <= lo): two 64-bit halves, a shift and a select each, no branches.
+__device__ __forceinline__ uint64_t low_bytes64(int k)  // bytes [0, k) of 8, 0 <= k <= 8
+{
+    return k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1ull);
+}
+__device__ __forceinline__ u32x4 word_byte_range(int lo, int hi)
+{
+    const int l0 = lo < 8 ? lo : 8, h0 = hi < 8 ? hi : 8;
+    const int l1 = lo > 8 ? lo - 8 : 0, h1 = hi > 8 ? hi - 8 : 0;
+    const uint64_t a = low_bytes64(h0) & ~low_bytes64(l0);
+    const uint64_t b = low_bytes64(h1) & ~low_bytes64(l1);
+    return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
 inline kmws_status hip_status(hipError_t e)
 {
     return e == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
