@@ -90,6 +90,24 @@ def placed_buffer(torch, kmws, span: int):
     return arena, view, rec
 
 
+def verify_sparse(torch, src, src_off, lens, dst, dst_off, frames_per_chunk=20000):
+    """dst[dst_off[i] : +lens[i]] == src[src_off[i] : +lens[i]] for every frame (payloads
+    where they lie, e.g. in a wire image), checked by index gathers in chunks."""
+    dev = src.device
+    for a in range(0, len(lens), frames_per_chunk):
+        b = min(len(lens), a + frames_per_chunk)
+        ln = torch.from_numpy(lens[a:b]).to(dev)
+        tot = int(ln.sum())
+        if tot == 0:
+            continue
+        rel = torch.arange(tot, device=dev) - torch.repeat_interleave(torch.cumsum(ln, 0) - ln, ln)
+        so = torch.repeat_interleave(torch.from_numpy(src_off[a:b].astype(np.int64)).to(dev), ln)
+        do = torch.repeat_interleave(torch.from_numpy(np.asarray(dst_off[a:b], dtype=np.int64)).to(dev), ln)
+        if not torch.equal(src[so + rel], dst[do + rel]):
+            return False
+    return True
+
+
 def timed(torch, fn, reps):
     ts = []
     for _ in range(reps):
@@ -150,12 +168,31 @@ def cfg3(reps: int, gib: float):
     ok = verify_dense(torch, src, src_off, lens, dst, dst_off)
     enc_bytes = 2 * P + H + 26 * n
     dec_bytes = 2 * P + H + 51 * n
+    # decode in place, as kuma does (WSHandler.cpp:247-250): unpack, then unmask the
+    # payloads where they lie in the wire (kmws_unmask_batch on the unpacked descriptors)
+    ws_m = kmws.Workspace(kmws.unmask_workspace_size(P + H))
+    sched = kmws.unmask_autotune(wire, out_desc, ws_m, P + H)  # this batch's schedule (payload unchanged)
+    kmws.unmask_batch(wire, out_desc, ws_m, P + H)  # one pass: unmasked, verified below
+    torch.cuda.synchronize()
+    ok_in_place = ws_m.status() == 0 and verify_sparse(torch, src, src_off, lens, wire, out_desc[:, 0].cpu().numpy())
+    t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), 2 * (reps // 2) + 2)
+
+    def decode_in_place():
+        kmws.unpack_headers(wire, hdr_off, kmws.SERVER, out_desc, out_flags, out_err, ws_u, wire_len=P + H)
+        kmws.unmask_batch(wire, out_desc, ws_m, P + H)
+
+    t_dip = timed(torch, decode_in_place, 2 * (reps // 2) + 2)  # even: the wire ends as it started
+    ok = ok and ok_in_place
     return {"config": "cfg3", "frames": n, "payload_bytes": P, "header_bytes": H,
             "encode": {"ms": t_enc * 1e3, "payload_GiB_s": P / t_enc / 2**30,
                        "alg_GB_s": enc_bytes / t_enc / 1e9, "hbm_frac": enc_bytes / t_enc / 8e12},
             "decode_unpack_gather": {"ms": t_dec * 1e3, "payload_GiB_s": P / t_dec / 2**30,
                                      "alg_GB_s": dec_bytes / t_dec / 1e9, "hbm_frac": dec_bytes / t_dec / 8e12},
             "unpack_only": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
+            "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30, "schedule": sched,
+                                "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
+            "decode_unpack_in_place": {"ms": t_dip * 1e3, "payload_GiB_s": P / t_dip / 2**30,
+                                       "hbm_frac": (2 * P + H + 16 * n + 35 * n) / t_dip / 8e12},
             "roundtrip_payload_GiB_s": P / (t_enc + t_dec) / 2**30, "verified": bool(ok),
             "note": "decode is descriptor-indexed: header offsets = the receiver's host parse (here wire_off)"}
 
