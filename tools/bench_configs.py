@@ -181,14 +181,39 @@ def cfg3(reps: int, gib: float):
         kmws.unpack_headers(wire, hdr_off, kmws.SERVER, out_desc, out_flags, out_err, ws_u, wire_len=P + H)
         kmws.unmask_batch(wire, out_desc, ws_m, P + H)
 
-    t_dip = timed(torch, decode_in_place, 2 * (reps // 2) + 2)  # even: the wire ends as it started
+    t_dip = timed(torch, decode_in_place, 2 * (reps // 2) + 2)  # even: the wire stays unmasked
+    kmws.unmask_batch(wire, out_desc, ws_m, P + H)  # back to the masked wire image
     ok = ok and ok_in_place
+    # encode in kuma's iovec form (sendWsFrame, WebSocketImpl.cpp:381-436): headers packed into
+    # 16-B slots (kmws_pack_headers), payloads masked in place where they lie (kmws_unmask_batch)
+    hslots = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    hlen = torch.empty(n, dtype=torch.uint8, device=dev)
+    woff2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ws_h = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    ws_s = kmws.Workspace(kmws.unmask_workspace_size(src_bytes))
+    sched_s = kmws.unmask_autotune(src, descs, ws_s, src_bytes)
+
+    def encode_iovec():
+        kmws.pack_headers(descs, fl, hslots, hlen, woff2, ws_h)
+        kmws.unmask_batch(src, descs, ws_s, src_bytes)
+
+    encode_iovec()  # one pass: every payload masked in place -> equal to the wire image's payloads
+    torch.cuda.synchronize()
+    woff_h = wire_off.cpu().numpy()
+    ok_iov = (ws_s.status() == 0 and torch.equal(woff2, wire_off) and
+              verify_sparse(torch, wire, woff_h[:n] + hl, lens, src, src_off) and            # masked payloads
+              verify_sparse(torch, wire, woff_h[:n], hl.astype(np.int64), hslots, 16 * np.arange(n)))  # headers
+    t_iov = timed(torch, encode_iovec, 2 * (reps // 2) + 1)  # odd: the payloads end unmasked, as they started
+    ok = ok and ok_iov
     return {"config": "cfg3", "frames": n, "payload_bytes": P, "header_bytes": H,
             "encode": {"ms": t_enc * 1e3, "payload_GiB_s": P / t_enc / 2**30,
                        "alg_GB_s": enc_bytes / t_enc / 1e9, "hbm_frac": enc_bytes / t_enc / 8e12},
             "decode_unpack_gather": {"ms": t_dec * 1e3, "payload_GiB_s": P / t_dec / 2**30,
                                      "alg_GB_s": dec_bytes / t_dec / 1e9, "hbm_frac": dec_bytes / t_dec / 8e12},
             "unpack_only": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
+            "encode_iovec_in_place": {"ms": t_iov * 1e3, "payload_GiB_s": P / t_iov / 2**30, "schedule": sched_s,
+                                      "hbm_frac": (2 * P + 59 * n) / t_iov / 8e12,
+                                      "note": "kmws_pack_headers (16-B header slots) + in-place mask of the payloads"},
             "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30, "schedule": sched,
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
             "decode_unpack_in_place": {"ms": t_dip * 1e3, "payload_GiB_s": P / t_dip / 2**30,
