@@ -448,6 +448,18 @@ def cfg4(reps: int, messages: int, placed: bool = True):
     ws_h = kmws.Workspace(kmws.pack_headers_workspace_size(n))
     t_hdr = timed(torch, lambda: kmws.pack_headers(descs, fl16, hslots, hlen, woff2, ws_h), reps)
     assert torch.equal(woff2, wire_off) and torch.equal(hslots.view(n, 16)[:, :8], wire[:P + H].view(n, L + 8)[:, :8])
+    # encode in kuma's iovec form: the header-only pack + the fragments masked in place where they lie
+    ws_s = kmws.Workspace(kmws.unmask_workspace_size(P))
+    sched_s = kmws.unmask_autotune(src, descs, ws_s, P)
+
+    def encode_iovec():
+        kmws.pack_headers(descs, fl16, hslots, hlen, woff2, ws_h)
+        kmws.unmask_batch(src, descs, ws_s, P)
+
+    encode_iovec()  # one pass: fragments masked, equal to the wire image's payloads
+    torch.cuda.synchronize()
+    ok_iov = ws_s.status() == 0 and bool(torch.equal(src[:P].view(n, L), wire[:P + H].view(n, L + 8)[:, 8:]))
+    t_iov = timed(torch, encode_iovec, 2 * (reps // 2) + 1)  # odd: the fragments end unmasked, as they started
     out_desc = torch.empty((n, 2), dtype=torch.int64, device=dev)
     out_flags = torch.empty(n, dtype=torch.int16, device=dev)
     out_err = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -497,6 +509,9 @@ def cfg4(reps: int, messages: int, placed: bool = True):
     return {"config": "cfg4", "messages": messages, "frames": n, "payload_bytes": P,
             "pack": {"ms": t_pack * 1e3, "Mheaders_s": n / t_pack / 1e6, "payload_GiB_s": P / t_pack / 2**30,
                      "hbm_frac": (2 * P + H + 26 * n) / t_pack / 8e12},
+            "encode_iovec_in_place": {"ms": t_iov * 1e3, "Mheaders_s": n / t_iov / 1e6, "schedule": sched_s,
+                                      "payload_GiB_s": P / t_iov / 2**30, "hbm_frac": (2 * P + 59 * n) / t_iov / 8e12,
+                                      "verified": ok_iov},
             "pack_headers_only": {"ms": t_hdr * 1e3, "Mheaders_s": n / t_hdr / 1e6,
                                   # desc 16 + flags 2 in, slot 16 + length 1 + wire offset 8 out
                                   "hbm_frac": 43 * n / t_hdr / 8e12},
@@ -505,7 +520,7 @@ def cfg4(reps: int, messages: int, placed: bool = True):
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12, "placed": placed_rec},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
             "device_header_walk_by_streams": walk,
-            "verified": verified}
+            "verified": verified and ok_iov}
 
 
 # ------------------------------------------------------------------ e2e
