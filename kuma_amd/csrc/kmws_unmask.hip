@@ -16,6 +16,13 @@
 // of traffic per payload byte + 16 B per descriptor; no MFMA.
 #include "kmws_common.hpp"
 
+// Uncapped split grids (batches of frames shorter than a tile, the LDS-staged
+// path) load the tile's descriptors before its payload: cfg4's in-place unmask
+// 80.3-80.4 -> 81.7-82.2 % (profiles/r02bt_unmask_desc_prefetch_ab.txt).  0 = off.
+#ifndef KMWS_UNMASK_PRE
+#define KMWS_UNMASK_PRE 1
+#endif
+
 namespace kmws {
 
 // Each lane owns V consecutive-block words: word w = tid + kBlock * i.
@@ -71,7 +78,8 @@ template <int V, bool FULL, bool TWO = false>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
                                             const kmws_desc* __restrict__ d, uint32_t n,
                                             const uint32_t* __restrict__ map, uint32_t tile, bool ok,
-                                            const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key)
+                                            const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key,
+                                            const u32x4* pre = nullptr)
 {
     using Cfg = UnmaskCfg<V>;
     const int tid = threadIdx.x;
@@ -146,11 +154,11 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
     u32x4 m[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) m[i] = u32x4{0, 0, 0, 0};
-    for (;;) {
-        const uint32_t fi = f + (uint32_t)tid;
+    // One round: lane tid holds descriptor f + tid (`have`: it exists and can
+    // overlap the tile); returns how many were staged.
+    auto round = [&](bool have, const u32x4& x) -> int {
         int valid = 0;
-        if (fi < n && fi <= flast) {  // no descriptor loads past the tile's last frame
-            const u32x4 x = *reinterpret_cast<const u32x4*>(d + fi);  // one 16-B load
+        if (have) {
             const uint64_t off = (uint64_t)x.x | ((uint64_t)x.y << 32);
             if (off < tile_hi) {
                 valid = 1;
@@ -186,8 +194,17 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
             }
         }
         __syncthreads();  // every lane done reading this round's LDS (also before a next tile reuses it)
-        if (cnt < Cfg::kCap) break;
+        return cnt;
+    };
+    // no descriptor loads past the tile's last frame; the first round's may
+    // have been issued before the payload loads (`pre`): then no wait here
+    // covers the payload
+    auto have_f = [&]() { return f + (uint32_t)tid < n && f + (uint32_t)tid <= flast; };
+    auto load_f = [&]() { return have_f() ? *reinterpret_cast<const u32x4*>(d + f + tid) : u32x4{0, 0, 0, 0}; };
+    int cnt = pre ? round(have_f(), *pre) : round(have_f(), load_f());
+    while (cnt == Cfg::kCap) {
         f += Cfg::kCap;
+        cnt = round(have_f(), load_f());
     }
 #pragma unroll
     for (int i = 0; i < V; ++i) {
@@ -269,6 +286,21 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     }
     const uint64_t lo = (uint64_t)tile * Cfg::kTile;
     u32x4 v[V];
+#if KMWS_UNMASK_PRE
+    if constexpr (!TWO) {
+        // the tile's descriptors first: their wait then counts only them, not the
+        // payload loads issued after them (vmcnt is one in-order queue)
+        const uint32_t f = map[tile], fl = map[tile + 1];
+        const uint32_t fi = f + threadIdx.x;
+        u32x4 pre = u32x4{0, 0, 0, 0};
+        if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
+        load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
+        __builtin_amdgcn_sched_barrier(0);
+        finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                  s_key, &pre);
+        return;
+    }
+#endif
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
     finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
