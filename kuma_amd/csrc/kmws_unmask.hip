@@ -111,7 +111,8 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
     // the payload loads are still in flight (built word by word between the
     // stores, it delayed each boundary tile's stores by ~12 %: the two-frame
     // path replaced by a plain XOR ran the packed wire at the aligned rate,
-    // profiles/r02bf_*).  Words whose mask is zero (headers, gaps) are not stored.
+    // profiles/r02bj_unmask_two_frame_ab.txt).  Words whose mask is zero (headers,
+    // gaps) are not stored.
     if (TWO && FULL && flast <= f + 1 && f < n) {
         const kmws_desc d1 = flast > f && flast < n ? d[flast] : kmws_desc{~0ull, 0u, 0u};
         const uint32_t r0 = rot_key(d0.key, d0.off), r1 = rot_key(d1.key, d1.off);
