@@ -83,6 +83,19 @@ def layout(kind, rng):
         starts = np.cumsum(np.concatenate([[0], gaps + lens]))
         offs = (starts[:-1] + gaps).astype(np.uint64)
         total = int(starts[-1]) + 11
+    elif kind == "long_gaps":  # regions >= one tile (capped grids, two-frame path): every header-gap size
+        n = 80                   # around a boundary, some frames ending exactly on a tile edge
+        gaps = rng.choice([0, 1, 2, 4, 8, 10, 14, 15, 16, 17, 31, 1024], size=n)
+        lens = rng.integers(16384, 70000, size=n)
+        offs = np.zeros(n, dtype=np.uint64)
+        pos = 0
+        for i in range(n):
+            pos += int(gaps[i])
+            offs[i] = pos
+            if i % 5 == 4:  # end on the next tile edge at least 16 KiB away
+                lens[i] = (pos + 16384 + 16383) // 16384 * 16384 - pos
+            pos += int(lens[i])
+        total = pos + 9
     else:
         raise ValueError(kind)
     keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
@@ -91,7 +104,7 @@ def layout(kind, rng):
     return buf, make_descs(offs, lens, keys)
 
 
-KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs", "sparse_gaps"]
+KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs", "sparse_gaps", "long_gaps"]
 
 
 @pytest.mark.parametrize("kind", KINDS)
