@@ -103,8 +103,13 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+TEMPORAL_STORES = 1 << 30  # KMWS_SCHED_TEMPORAL_STORES (include/kmws_gpu.h)
+
+
 def schedule_kernel(schedule: int) -> str:
     """Kernel that carries the unmask for a kmws_unmask_schedule() code."""
+    if schedule & TEMPORAL_STORES:
+        return "unmask_split_kernel"
     if schedule in (0, 2, 3, 4, 5):
         return "unmask_split_kernel"
     if schedule == 1:
@@ -113,6 +118,8 @@ def schedule_kernel(schedule: int) -> str:
 
 
 def schedule_name(schedule: int) -> str:
+    if schedule & TEMPORAL_STORES:
+        return schedule_name(schedule & ~TEMPORAL_STORES) + ", temporal payload stores"
     if schedule == 0:
         return "one block per 16 KiB tile, 2 groups of 4 XCDs, runs of 16 tiles per XCD in the group's half"
     if schedule == 4:

@@ -228,7 +228,10 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * the XCDs in 2 groups, each dealing runs of 16 tiles inside its own half of
  * the span (0, the default), in order (1), tiles dealt over 2 (2), 8 (3) or 4 (5)
  * far-apart parts of the span, runs of 16 tiles per XCD (4); >= 64: a
- * persistent grid of that many blocks (+1: the pipelined grid).  kmws_unmask_schedule() reports the current one. */
+ * persistent grid of that many blocks (+1: the pipelined grid); codes 0, 2-5 with bit 30 set
+ * (KMWS_SCHED_TEMPORAL_STORES): the same split grids storing the payload with temporal stores
+ * (split 4 and split 8 are timed that way too).  kmws_unmask_schedule() reports the current one. */
+#define KMWS_SCHED_TEMPORAL_STORES (1 << 30)
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
 int kmws_unmask_schedule(void);

@@ -16,6 +16,7 @@
 // of traffic per payload byte + 16 B per descriptor; no MFMA.
 #include "kmws_common.hpp"
 
+
 // Uncapped split grids (batches of frames shorter than a tile, the LDS-staged
 // path) load the tile's descriptors before its payload: cfg4's in-place unmask
 // 80.3-80.4 -> 81.7-82.2 % (profiles/r02bt_unmask_desc_prefetch_ab.txt).  0 = off.
@@ -24,6 +25,19 @@
 #endif
 
 namespace kmws {
+
+// Payload store of a tile word: non-temporal (streams past the L2; the
+// default) or temporal (NT = false: the line stays in L2 and is written back
+// on eviction).  Which one streams faster depends on the batch's layout: on an
+// aligned arena temporal stores ran +0.3-1.0 points, on a packed wire image
+// they lost 1.6-7 (profiles/r02bz_unmask_store_policy_ab.txt), so the policy
+// is part of the schedule the autotune times on the caller's batch.
+template <bool NT>
+__device__ __forceinline__ void store_word(const u32x4& val, u32x4* p)
+{
+    if constexpr (NT) __builtin_nontemporal_store(val, p);
+    else *p = val;
+}
 
 // Each lane owns V consecutive-block words: word w = tid + kBlock * i.
 template <int V>
@@ -74,7 +88,7 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint
 }
 
 // Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
-template <int V, bool FULL, bool TWO = false>
+template <int V, bool FULL, bool TWO = false, bool NT = true>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
                                             const kmws_desc* __restrict__ d, uint32_t n,
                                             const uint32_t* __restrict__ map, uint32_t tile, bool ok,
@@ -97,7 +111,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-            if (ok) __builtin_nontemporal_store(v[i] ^ r, reinterpret_cast<u32x4*>(base + a));
+            if (ok) store_word<NT>(v[i] ^ r, reinterpret_cast<u32x4*>(base + a));
         }
         return;
     }
@@ -145,7 +159,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
             if (ok && (m[i].x | m[i].y | m[i].z | m[i].w) != 0u)
-                __builtin_nontemporal_store(v[i] ^ m[i], reinterpret_cast<u32x4*>(base + a));
+                store_word<NT>(v[i] ^ m[i], reinterpret_cast<u32x4*>(base + a));
         }
         return;
     }
@@ -212,7 +226,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
         const u32x4 mm = m[i];
         if (ok && (FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
-            __builtin_nontemporal_store(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a));
+            store_word<NT>(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a));
     }
 }
 
@@ -253,7 +267,7 @@ __global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __rest
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
 // its own runs).
-template <int V, bool TWO = false>
+template <int V, bool TWO = false, bool NT = true>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
@@ -297,14 +311,15 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
         if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
         load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
-                                  s_key, &pre);
+        finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                      s_key, &pre);
         return;
     }
 #endif
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
+    finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                  s_key);
 }
 
 // Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
@@ -667,7 +682,7 @@ static uint32_t resident_blocks(const void* kernel)
     return (uint32_t)(cus * per);
 }
 
-template <int V>
+template <int V, bool NT = true>
 static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                       const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
                                       uint32_t c = 0, uint32_t w = 1)
@@ -687,11 +702,11 @@ static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_d
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
         if (lds_pad)
-            hipLaunchKernelGGL((unmask_split_kernel<V, true>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s, base, descs,
-                               n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+            hipLaunchKernelGGL((unmask_split_kernel<V, true, NT>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s, base,
+                               descs, n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
         else
-            hipLaunchKernelGGL(unmask_split_kernel<V>, dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs, n, map,
-                               head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+            hipLaunchKernelGGL((unmask_split_kernel<V, false, NT>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs,
+                               n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
@@ -708,6 +723,10 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
     return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
 }
 
+// Flag on schedule codes 0, 2, 3, 4, 5: payload stores temporal instead of
+// non-temporal (store_word).
+constexpr uint32_t kSchedTemporal = 1u << 30;
+
 // Schedule code, one block per 16 KiB tile: the XCDs in 2 groups of 4, each
 // group dealing runs of 16 tiles to its XCDs inside its own half of the span
 // (0, the default), in order (1), tiles dealt over 2 parts of the span (2) or
@@ -717,6 +736,16 @@ static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* 
 static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                    const void* workspace, size_t ws_bytes, hipStream_t s)
 {
+    if (code & kSchedTemporal) {  // the same split schedules with temporal payload stores
+        switch (code & ~kSchedTemporal) {
+        case 0: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u, 2u);
+        case 2: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 2u);
+        case 3: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u);
+        case 4: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
+        case 5: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 4u);
+        default: return KMWS_ERR_INVALID_PARAM;
+        }
+    }
     if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u, 2u);
     if (code == 4) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
     if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
@@ -820,7 +849,9 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     // depends on where the batch lies in HBM, on its frame layout and on the
     // blocks in flight (profiles/r01f_unmask_placement.txt; at 2 blocks per CU
     // 4 parts led with 85.3 %, profiles/r02al_unmask_schedules_2bpc.txt)
-    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u};
+    // (+ split 4 and split 8 with temporal stores: faster on aligned arenas,
+    // slower on packed wire images, profiles/r02bz_unmask_store_policy_ab.txt)
+    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u, 5u | kSchedTemporal, 3u | kSchedTemporal};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {

@@ -108,7 +108,8 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 66, 65537, 2097152])
+@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 66, 65537, 2097152,
+                                     1 << 30, 2 | 1 << 30, 3 | 1 << 30, 4 | 1 << 30, 5 | 1 << 30])  # temporal stores
 def test_unmask_parity(torch_dev, kind, variant):
     rng = np.random.default_rng(zlib.crc32(f"{kind}-{variant}".encode()))
     buf, descs = layout(kind, rng)
@@ -212,7 +213,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
     ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
-    assert choice in (0, 1, 2, 3, 4, 5) and kmws.unmask_schedule() == choice
+    assert choice in (0, 1, 2, 3, 4, 5, 5 | 1 << 30, 3 | 1 << 30) and kmws.unmask_schedule() == choice
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
