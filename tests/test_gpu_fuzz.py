@@ -25,7 +25,8 @@ from oracle import oracle as orc
 
 pytestmark = pytest.mark.gpu
 BUDGET = float(os.environ.get("KMWS_FUZZ_SECONDS", "8"))
-SCHEDULES = [None, 0, 23, 21, 27, 36, 3, 10]  # product default, in order, splits, XCD runs, persistent grids
+SCHEDULES = [None, 0, 23, 21, 27, 36, 3, 10,  # product default, in order, splits, XCD runs, persistent grids
+             5 | 1 << 30, 3 | 1 << 30]         # split 4 / split 8 with temporal stores
 
 
 @pytest.fixture(scope="module")
