@@ -230,7 +230,7 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * far-apart parts of the span, runs of 16 tiles per XCD (4); >= 64: a
  * persistent grid of that many blocks (+1: the pipelined grid); codes 0, 2-5 with bit 30 set
  * (KMWS_SCHED_TEMPORAL_STORES): the same split grids storing the payload with temporal stores
- * (split 4 and split 8 are timed that way too).  kmws_unmask_schedule() reports the current one. */
+ * (the autotune times every one of them that way too).  kmws_unmask_schedule() reports the current one. */
 #define KMWS_SCHED_TEMPORAL_STORES (1 << 30)
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);

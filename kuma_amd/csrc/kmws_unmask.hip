@@ -849,9 +849,11 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     // depends on where the batch lies in HBM, on its frame layout and on the
     // blocks in flight (profiles/r01f_unmask_placement.txt; at 2 blocks per CU
     // 4 parts led with 85.3 %, profiles/r02al_unmask_schedules_2bpc.txt)
-    // (+ split 4 and split 8 with temporal stores: faster on aligned arenas,
-    // slower on packed wire images, profiles/r02bz_unmask_store_policy_ab.txt)
-    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u, 5u | kSchedTemporal, 3u | kSchedTemporal};
+    // (+ the split schedules with temporal stores: faster on aligned arenas,
+    // slower on packed wire images, profiles/r02bz_unmask_store_policy_ab.txt;
+    // with them split 2 leads on the aligned arena, r02cj_unmask_ts_candidates_ab.txt)
+    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u, 5u | kSchedTemporal, 3u | kSchedTemporal,
+                                    2u | kSchedTemporal, 0u | kSchedTemporal, 4u | kSchedTemporal};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {

@@ -213,7 +213,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
     ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
-    assert choice in (0, 1, 2, 3, 4, 5, 5 | 1 << 30, 3 | 1 << 30) and kmws.unmask_schedule() == choice
+    assert (choice in (0, 1, 2, 3, 4, 5) or (choice & ~(1 << 30)) in (0, 2, 3, 4, 5)) and kmws.unmask_schedule() == choice
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
