@@ -35,25 +35,31 @@ DESC_BYTES = 16
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="GPUs (ranks) of this node. Without WORLD_SIZE in the environment bench.py starts the N "
+                        "rank processes itself (one per GPU, before any GPU call); under torchrun WORLD_SIZE "
+                        "must equal N")
     p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg1"],
                    help="cfg2 (default): the headline device-resident unmask; cfg1: kuma's CPU case "
                         "(1,000 x 4 KiB frames in 64 KiB reads) with its cpu_baseline")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
-    p.add_argument("--job-frames", type=int, default=0,
-                   help="strong scaling: a fixed job of this many frames split over the ranks (configs[4]: 10485760); "
-                        "0 = weak scaling, --frames per GPU")
+    p.add_argument("--job-frames", type=int, default=None,
+                   help="strong scaling: a fixed job of this many frames split over the ranks (configs[4]: 10485760, "
+                        "the default for N > 1); 0 = weak scaling, --frames per GPU (the default for N = 1: cfg2)")
     p.add_argument("--max-batch-frames", type=int, default=1310720,
                    help="largest resident batch per GPU (80 GiB of 64 KiB frames); larger shards run as sub-batches")
     p.add_argument("--frame-len", type=int, default=65536)
-    p.add_argument("--variant", type=int, default=-1, help="tile variant (-1 = product default)")
+    p.add_argument("--schedule", type=int, default=-1,
+                   help="pin an unmask schedule code (include/kmws_gpu.h KMWS_SCHED_*); -1 = autotune the batch")
     p.add_argument("--seed", type=int, default=0x6B756D61)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core os.sched_getaffinity grants")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-autotune", action="store_true", help="skip kmws_unmask_autotune (keep the default schedule)")
+    p.add_argument("--no-plain", action="store_true",
+                   help="skip the second measurement of the same schedule on a plain torch.empty batch")
     p.add_argument("--placement", default="probe", choices=["probe", "plain"],
                    help="probe: carve the batch from a larger contiguous HBM arena at the offset where a timed "
                         "split-8 unmask runs fastest (DESIGN.md sec.4 'placement'); plain: torch.empty(span)")
@@ -64,10 +70,27 @@ def parse():
     return p.parse_args()
 
 
+def host_cores():
+    """(cores this process may run on, the cgroup CPU quota in cores or None)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
 def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
     """Times the oracle (kuma's byte loop, WSHandler.cpp:303-310, restated in
     oracle/kmws_oracle.c) on host cores over a bounded sample of the same
-    workload: 4096 x frame_len frames, repeated for ~`seconds`."""
+    workload: 16384 x frame_len frames (1 GiB), repeated for ~`seconds`, one
+    thread per core (SURVEY 8 d: kuma's loop on all host cores)."""
     import numpy as np
     from oracle import oracle as orc
     n = 16384  # 1 GiB of 64 KiB frames: 4x the host's L3, so the sample streams from DRAM
@@ -86,7 +109,9 @@ def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
         if el >= seconds:
             break
     gib = passes * n * frame_len / 2**30
+    aff, quota = host_cores()
     return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "affinity_cores": aff, "cgroup_cpu_quota_cores": quota,
             "sample": f"{n} x {frame_len} B frames ({n * frame_len >> 20} MiB), in-place unmask with the "
                       f"oracle's restatement of WSHandler::handleDataMask (scalar byte loop, gcc -O3), "
                       f"{threads} threads, {passes} passes in {el:.1f} s",
@@ -103,33 +128,22 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-TEMPORAL_STORES = 1 << 30  # KMWS_SCHED_TEMPORAL_STORES (include/kmws_gpu.h)
-
-
-def schedule_kernel(schedule: int) -> str:
-    """Kernel that carries the unmask for a kmws_unmask_schedule() code."""
-    if schedule & TEMPORAL_STORES:
-        return "unmask_split_kernel"
-    if schedule in (0, 2, 3, 4, 5):
-        return "unmask_split_kernel"
-    if schedule == 1:
-        return "unmask_tiles_kernel"
-    return "unmask_pipe_kernel" if schedule & 1 else "unmask_persist_kernel"
+TEMPORAL_STORES, NT_STORES = 1 << 30, 1 << 29  # KMWS_SCHED_* store bits (include/kmws_gpu.h)
+UNMASK_KERNEL = "unmask_split_kernel"
 
 
 def schedule_name(schedule: int) -> str:
+    kind = {0: "one block per 16 KiB tile, 2 groups of 4 XCDs, runs of 16 tiles per XCD in the group's half",
+            1: "one block per 16 KiB tile, in order",
+            2: "one block per 16 KiB tile, tiles dealt over 2 parts of the span",
+            3: "one block per 16 KiB tile, tiles dealt over 8 parts of the span",
+            4: "one block per 16 KiB tile, runs of 16 tiles per XCD",
+            5: "one block per 16 KiB tile, tiles dealt over 4 parts of the span"}.get(schedule & 0xFF, "?")
     if schedule & TEMPORAL_STORES:
-        return schedule_name(schedule & ~TEMPORAL_STORES) + ", temporal payload stores"
-    if schedule == 0:
-        return "one block per 16 KiB tile, 2 groups of 4 XCDs, runs of 16 tiles per XCD in the group's half"
-    if schedule == 4:
-        return "one block per 16 KiB tile, runs of 16 tiles per XCD"
-    if schedule in (2, 3, 5):
-        return f"one block per 16 KiB tile, tiles dealt over {dict([(2, 2), (3, 8), (5, 4)])[schedule]} parts of the span"
-    if schedule == 1:
-        return "one block per 16 KiB tile, in order"
-    kind = "pipelined persistent grid" if schedule & 1 else "persistent grid-stride"
-    return f"{kind}, {schedule & ~1} blocks"
+        return kind + ", temporal payload stores"
+    if schedule & NT_STORES:
+        return kind + ", non-temporal payload stores"
+    return kind + ", automatic store policy (temporal on tile-aligned batches)"
 
 
 def traffic_from_profile(frames: int, frame_len: int, kernel: str, schedule=None):
@@ -342,6 +356,7 @@ def run_cfg1(reps: int = 10) -> dict:
 
 
 PLACEMENT_STEP = 16 << 30
+CFG5_JOB_FRAMES = 10485760  # BASELINE configs[4]
 
 
 def placement_slack(span: int, free: int, want: int) -> int:
@@ -368,7 +383,7 @@ def place_batch(kmws, torch, dev, span, slack):
         arena = kmws.Arena(span + slack, device=dev.index)
     except RuntimeError as e:
         return None, None, {"kind": "plain torch.empty", "why": str(e)}
-    off, probe = kmws.arena_place(arena, span, PLACEMENT_STEP)  # kmws_arena_place: timed split-8 passes
+    off, probe = kmws.arena_place(arena, span, PLACEMENT_STEP)  # kmws_arena_place: timed split-4/8 passes
     pick = off >> 30
     rec = {"kind": "offset in a contiguous arena, picked by kmws_arena_place (timed probe: best of split 4 and split 8 per offset)",
            "arena_GiB": (span + slack) >> 30, "contiguous": arena.contiguous, "offset_GiB": pick,
@@ -376,22 +391,115 @@ def place_batch(kmws, torch, dev, span, slack):
     return arena, arena.tensor[pick << 30:(pick << 30) + span], rec
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script (one
+    per GPU) with the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for all of them.  The parent
+    never touches the GPU (it only forks children, no exec from a GPU process).
+    Rank 0 prints the JSON line; returns the first non-zero exit status."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"bench: rank exit codes {codes}", file=sys.stderr)
+    return bad[0] if bad else 0
+
+
+def time_steps(kmws, torch, stream, step, steps, world, dist):
+    """Barrier + synchronize, `steps` timed steps with HIP events around each
+    unmask launch on the launch stream, synchronize + barrier.  Returns (wall s,
+    summed event ms)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(*evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0, sum(e0.elapsed_time(e1) for e0, e1 in evs)
+
+
+def plain_rate(kmws, torch, dev, n, L, descs, ws, schedule, seed, steps, warmup, stream):
+    """The same batch and schedule on a plain torch.empty allocation (no arena,
+    no placement probe): fraction of the 8 TB/s peak from the HIP events of
+    `steps` timed launches, every byte verified.  Also the autotune's pick on
+    that allocation and its rate."""
+    span = n * L
+    base = torch.empty(span, dtype=torch.uint8, device=dev)
+    kmws.fill_synthetic(base, seed)
+    out = {}
+    for label, tune in (("same_schedule", False), ("autotuned", True)):
+        if tune:
+            sched = kmws.unmask_autotune(base, descs, ws, span)
+        else:
+            kmws.unmask_set_schedule(ws, descs, span, schedule)
+            sched = schedule
+        kmws.unmask_plan(descs, ws, span)
+        for _ in range(warmup):
+            kmws.unmask_apply(base, descs, ws, span)
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            kmws.unmask_apply(base, descs, ws, span)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / steps
+        out[label] = {"schedule": sched, "kernel_ms": round(ms, 4),
+                      "frac": round(n * (2 * L + DESC_BYTES) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if (warmup + steps) % 2 == 1:  # leave the batch masked, as generated
+            kmws.unmask_apply(base, descs, ws, span)
+    kmws.unmask_batch(base, descs, ws, span)
+    mism = kmws.check_unmasked(base, seed, descs)
+    kmws.unmask_set_schedule(ws, descs, span, schedule)  # the placed batch's schedule, as before
+    del base
+    torch.cuda.empty_cache()
+    out["byte_mismatches"] = mism
+    return out
+
+
 def main():
     a = parse()
     if a.config == "cfg1":
         print(json.dumps(run_cfg1(max(a.steps, 10))), flush=True)
         return
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    world = int(env_world or "1")
+    if world != a.gpus:
+        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU, the two must agree")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    job_frames = a.job_frames if a.job_frames is not None else (CFG5_JOB_FRAMES if world > 1 else 0)
+
     import torch
     import torch.distributed as dist
     from kuma_amd import kmws
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench: no GPU visible; the HIP path has no CPU fallback")
     dev = torch.device("cuda", local % ndev)  # one GPU per rank; modulo only when rehearsing on fewer GPUs
+    shared_gpu = world > ndev  # a rehearsal: several ranks on one GPU (gloo)
     torch.cuda.set_device(dev)
     if world > 1:
         if a.dist_backend == "nccl":
@@ -404,11 +512,12 @@ def main():
 
     from kuma_amd import shard
     L = a.frame_len
-    # The job: world x frames (weak scaling, default) or --job-frames J split over
-    # the ranks (strong scaling, BASELINE configs[4]: 10 M frames on 1..8 GPUs).
-    # Rank g owns global frames [lo, hi) (kuma_amd/shard.py); payload and keys are
-    # generated from global positions, so the shards are slices of one big job.
-    job = a.job_frames if a.job_frames else a.frames * world
+    # The job: world x frames (weak scaling, N = 1 default: cfg2) or a fixed job
+    # of J frames split over the ranks (strong scaling, BASELINE configs[4]: 10 M
+    # frames on 1..8 GPUs, the N > 1 default).  Rank g owns global frames [lo, hi)
+    # (kuma_amd/shard.py); payload and keys are generated from global positions,
+    # so the shards are slices of one big job.
+    job = job_frames if job_frames else a.frames * world
     g_lo, g_hi = shard.uniform_range(job, rank, world)
     # A shard larger than one resident batch runs as sub-batches (same count on
     # every rank), each generated on device untimed, then timed like one batch.
@@ -417,17 +526,18 @@ def main():
     span = n * L
     descs = torch.empty((n, 2), dtype=torch.int64, device=dev)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span), device=dev)
-    kmws.fill_uniform_descs(descs, L, L, (a.seed ^ 0x5EED) + g_lo)
     arena, placement = None, {"kind": "plain torch.empty"}
-    if a.placement == "probe":
+    if a.placement == "probe" and not shared_gpu:
         arena, base_all, placement = place_batch(kmws, torch, dev, span, a.placement_slack_gib << 30)
+    elif shared_gpu:
+        placement["why"] = f"{world} ranks share {ndev} GPU(s): rehearsal, no arena"
     if arena is None:
         base_all = torch.empty(span, dtype=torch.uint8, device=dev)
 
-    variant = None if a.variant < 0 else a.variant
     stream = torch.cuda.current_stream()
-    schedule = 0
+    schedule = a.schedule if a.schedule >= 0 else kmws.SCHED_GROUPED_RUNS
     elapsed, ev_ms, launches, alg_total, mismatches, st, done = 0.0, 0.0, 0, 0, 0, 0, 0
+    ranges = []
     for j, (b_lo, b_hi) in enumerate(batches):
         bn = b_hi - b_lo
         bspan = bn * L
@@ -436,47 +546,36 @@ def main():
         if bn:
             kmws.fill_uniform_descs(bdescs, L, L, (a.seed ^ 0x5EED) + b_lo)
             kmws.fill_synthetic(base, seed)
+            if a.schedule >= 0:
+                kmws.unmask_set_schedule(ws, bdescs, bspan, a.schedule)
+            elif j == 0 and not a.no_autotune:
+                # untimed, payload unchanged: picks this batch's faster unmask schedule
+                schedule = kmws.unmask_autotune(base, bdescs, ws, bspan)
+            elif not a.no_autotune:
+                kmws.unmask_set_schedule(ws, bdescs, bspan, schedule)  # same layout as batch 0
         torch.cuda.synchronize()
 
         def step(ev0=None, ev1=None):
             if bn == 0:
                 return
-            if variant is None:
-                kmws.unmask_plan(bdescs, ws, bspan)
-                if ev0 is not None:
-                    ev0.record(stream)
-                kmws.unmask_apply(base, bdescs, ws, bspan)
-                if ev1 is not None:
-                    ev1.record(stream)
-            else:
-                if ev0 is not None:
-                    ev0.record(stream)
-                kmws.unmask_batch(base, bdescs, ws, bspan, variant=variant)
-                if ev1 is not None:
-                    ev1.record(stream)
+            kmws.unmask_plan(bdescs, ws, bspan)
+            if ev0 is not None:
+                ev0.record(stream)
+            kmws.unmask_apply(base, bdescs, ws, bspan)
+            if ev1 is not None:
+                ev1.record(stream)
 
-        if j == 0 and bn and variant is None and not a.no_autotune:
-            # untimed, payload unchanged: picks this box's faster unmask schedule
-            schedule = kmws.unmask_autotune(base, bdescs, ws, bspan)
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(a.steps):
-            step(*evs[i])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed += time.perf_counter() - t0
+        wall, ms = time_steps(kmws, torch, stream, step, a.steps, world, dist)
+        elapsed += wall
         if bn:
-            ev_ms += sum(e0.elapsed_time(e1) for e0, e1 in evs)
+            ev_ms += ms
             launches += a.steps
             alg_total += a.steps * bn * (2 * L + DESC_BYTES)
         done += bn
+        ranges.append([b_lo, b_hi])
         st |= ws.status()
         if not a.no_verify and bn:
             if (a.warmup + a.steps) % 2 == 0:  # XOR twice is the identity: bring the batch to the unmasked state
@@ -487,55 +586,76 @@ def main():
     # full, n frames, when nb divides the shard)
     kern_ms = ev_ms / max(launches, 1)
     alg_bytes = alg_total // max(launches, 1)
+
+    plain = None
+    if world == 1 and not a.no_plain and arena is not None:
+        # the same schedule on a plain allocation: the headline is not a best-of-placements number alone
+        del base_all, base
+        arena = None
+        torch.cuda.empty_cache()
+        b_lo, b_hi = batches[0]
+        plain = plain_rate(kmws, torch, dev, b_hi - b_lo, L, descs[:b_hi - b_lo], ws, schedule,
+                           a.seed + (b_lo * L >> 3), a.steps, a.warmup, stream)
+        if not a.no_verify:
+            mismatches += plain["byte_mismatches"]
+
+    # gather per-rank facts on rank 0: elapsed, kernel time, mismatches, frame ranges
+    per_rank = [{"rank": rank, "device": dev.index, "frames": [g_lo, g_hi], "sub_batches": ranges,
+                 "elapsed_s": round(elapsed, 4), "kernel_ms": round(kern_ms, 4), "byte_mismatches": mismatches}]
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        t = torch.tensor([mismatches, st], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(t)
+        mismatches, st = int(t[0]), int(t[1])
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0])
+        per_rank = gathered
     if a.no_verify:
         mismatches = None
-    elif world > 1:
-        t = torch.tensor([mismatches], dtype=torch.int64, device=coll_dev)
-        dist.all_reduce(t)
-        mismatches = int(t[0])
 
     ms_per_step = elapsed * 1e3 / a.steps  # one step = one pass over the rank's shard
     total_payload = job * L
     value = total_payload * a.steps / elapsed / 2**30  # = shard.aggregate_rate over ranks (elapsed = max)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    kernel = schedule_kernel(schedule) if variant is None else f"kmws_unmask_batch_variant({variant})"
-    traffic = traffic_from_profile(n, L, kernel, schedule if variant is None else None)
+    traffic = traffic_from_profile(n, L, UNMASK_KERNEL, schedule)
 
     out = None
     if rank == 0:
         cpu = None
         if a.cpu_seconds > 0 and world == 1:
-            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+            thr = a.cpu_threads or host_cores()[0]
             cpu = cpu_baseline(a.cpu_seconds, thr, L, a.seed)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "strong" if a.job_frames else "weak", "vs_baseline": None, "dtype": "u8",
+            "higher_is_better": True, "scaling": "strong" if job_frames else "weak", "vs_baseline": None,
+            "dtype": "u8",
             "data": "synthetic (device-generated splitmix64 payload, per-frame random keys)",
             "config": {"workload": ("cfg5: fixed job of %d frames split over the GPUs (per-GPU frame partition), "
-                                    "device-resident in-place unmask" % job) if a.job_frames else
+                                    "device-resident in-place unmask" % job) if job_frames else
                                    "cfg2: 1 GPU device-resident in-place unmask of masked binary frames "
                                    "(aligned arena); N GPUs = per-GPU frame partition",
                        "frames_per_gpu": g_hi - g_lo, "frame_len": L, "total_frames": job,
                        "resident_batch_frames": n, "sub_batches": nb,
                        "layout": "aligned arena, frame i at i*frame_len",
                        "parallelism": f"frame-partition x{world} (no collective)",
-                       "tile_variant": "default" if variant is None else variant,
-                       "unmask_schedule": schedule_name(schedule),
+                       "dist_backend": a.dist_backend if world > 1 else None,
+                       "unmask_schedule": schedule, "unmask_schedule_name": schedule_name(schedule),
                        "placement": placement},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "frac_plain": plain["same_schedule"]["frac"] if plain else None,
                          "traffic": traffic,
-                         "kernel": kernel,
+                         "kernel": UNMASK_KERNEL,
                          "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
+            "plain_allocation": plain,
             "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /
                                          (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
             "verify": {"status_word": st, "byte_mismatches": mismatches},
+            "ranks": per_rank,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

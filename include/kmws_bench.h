@@ -1,0 +1,63 @@
+/*
+ * kmws_bench.h -- bench / test support entries of libkmws_gpu.so.
+ *
+ * Not part of the drop-in boundary (include/kmws_gpu.h): these allocate payload
+ * arenas, generate synthetic batches on the device and check them there, so
+ * bench.py and the GPU tests can build 64 GiB batches without host copies.
+ * Same conventions as kmws_gpu.h (kmws_status returns, device pointers,
+ * `void*` HIP streams).
+ */
+#ifndef KMWS_BENCH_H
+#define KMWS_BENCH_H
+
+#include "kmws_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- payload arenas ---- */
+
+/* Device memory for a batch arena, physically contiguous when the device can
+ * provide it (hipExtMallocWithFlags + hipDeviceMallocContiguous), else a plain
+ * hipMalloc.  Where an allocation lands in HBM decides how well the unmask
+ * schedule spreads its in-flight windows over the memory: contiguous arenas
+ * held 81-83 % of peak, plain 64 GiB allocations 76-83 % depending on the
+ * allocation.  *contiguous (optional) reports which one was
+ * obtained.  Free with kmws_arena_free.  Returns NULL on failure. */
+void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous);
+void  kmws_arena_free(void* p, int device);
+
+/* Placement probe for a long-lived batch region inside an arena: times in-place
+ * split-4 and split-8 unmasks of `span` bytes (uniform 64 KiB probe frames, each
+ * applied twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step,
+ * ... (offset + span <= arena_bytes) and returns the byte offset where the better
+ * of the two is fastest, or a negative kmws_status.  The split schedules run 76 % or 82-85 % of HBM
+ * peak depending on where the batch lies in physical HBM, which the kernel
+ * cannot see (DESIGN.md sec.4 "Placement").  frac_out (optional, max_out
+ * entries) receives each offset's rate as a fraction of 8 TB/s.  A setup call:
+ * allocates its probe descriptors and workspace, synchronizes the stream. */
+int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, uint64_t step, void* stream,
+                         float* frac_out, uint32_t max_out);
+
+/* ---- synthetic data + checks (bench / test support, device side) ---- */
+
+/* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */
+kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream);
+
+/* Uniform descriptors: desc i = {i*stride, len, key_i}, key_i = low 32 bits of
+ * splitmix64(key_seed + i). */
+kmws_status kmws_fill_uniform_descs(kmws_desc* descs, uint32_t n, uint64_t stride, uint32_t len,
+                                    uint64_t key_seed, void* stream);
+
+/* Independent byte-wise checker: counts bytes of base[0..bytes) that differ
+ * from synthetic(seed) XOR (the key byte of the covering frame, if any) into
+ * *mismatches (device u64, accumulated).  Descriptors must be sorted. */
+kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t seed,
+                                const kmws_desc* descs, uint32_t n,
+                                unsigned long long* mismatches, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMWS_BENCH_H */

@@ -20,8 +20,11 @@
  *    synchronous, pinned staging or zero-copy on caller-pinned memory.
  *  - device batch entries (kmws_*_batch, kmws_unpack_headers,
  *    kmws_gather_unmask): stream-ordered, no host sync, no allocation; all
- *    pointers are device pointers; workspace is caller-owned.  Set-up helpers
- *    (kmws_unmask_autotune, kmws_arena_*) may synchronize and allocate.
+ *    pointers are device pointers; workspace is caller-owned.  The one set-up
+ *    call, kmws_unmask_autotune, synchronizes.
+ *
+ * Bench / test support (arenas, synthetic batches, the device checker) lives
+ * in include/kmws_bench.h, outside this boundary.
  */
 #ifndef KMWS_GPU_H
 #define KMWS_GPU_H
@@ -136,25 +139,36 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
  * thread instead feeds every read of every connection with
  * kmws_decoder_feed_deferred (headers parsed and validated immediately, same
  * return values as kmws_decoder_feed; payloads copied into the batch) and
- * calls kmws_rx_batch_flush once per iteration: one GPU unmask over all
- * staged payloads, then every deferred callback in feed order (the
- * EventLoop::post pattern, kmapi.h:204-210).  Payload views point into the
- * batch and are valid during the callback; the caller's chunk is not
+ * once per iteration either calls kmws_rx_batch_flush -- one GPU unmask over
+ * all staged payloads, then every deferred callback in feed order -- or,
+ * asynchronously, kmws_rx_batch_submit (enqueues the unmask of the iteration's
+ * frames and returns at once) and kmws_rx_batch_poll at the next iterations
+ * (delivers the callbacks of every submitted generation whose unmask has
+ * finished, in submit order; wait != 0: all of them), so the GPU round trip
+ * overlaps the loop's socket reads (the EventLoop::post pattern,
+ * kmapi.h:204-210).  Payload views point into the batch (or the attached
+ * ring) and are valid during the callback; the caller's chunk is not
  * modified.  A callback returning nonzero ("destroyed") drops that decoder's
- * remaining frames of the flush.  Destroy a decoder only after a flush or
- * after kmws_rx_batch_discard. */
+ * remaining frames of the generation.  Destroy a decoder only after its
+ * frames were delivered or after kmws_rx_batch_discard (which also covers
+ * submitted generations).  Do not mix kmws_decoder_feed and deferred feeds on
+ * one decoder while its frames are pending. */
 typedef struct kmws_rx_batch kmws_rx_batch;
 kmws_rx_batch* kmws_rx_batch_create(int device);      /* NULL without a gfx950 device */
 void           kmws_rx_batch_destroy(kmws_rx_batch* b);
 int            kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_t* data, size_t len,
                                           kmws_frame_cb cb, void* user);
 int            kmws_rx_batch_flush(kmws_rx_batch* b);  /* frames delivered, or negative status */
-int            kmws_rx_batch_pending(const kmws_rx_batch* b);
-/* Optional pinned receive ring (hipHostMalloc / hipHostRegister) that the loop
- * reads sockets into: chunks fed from inside it are not copied -- their
- * masked payloads are unmasked in place there at flush (zero-copy), and the
- * callback views point into the ring.  The ring bytes fed since the last
- * flush must stay unmodified until that flush.  NULL detaches. */
+int            kmws_rx_batch_submit(kmws_rx_batch* b); /* frames submitted (0: none), or negative status */
+int            kmws_rx_batch_poll(kmws_rx_batch* b, int wait);  /* frames delivered, or negative status */
+int            kmws_rx_batch_pending(const kmws_rx_batch* b);   /* frames fed, not yet submitted */
+int            kmws_rx_batch_inflight(const kmws_rx_batch* b);  /* generations submitted, not yet delivered */
+/* Optional pinned receive ring (hipHostMalloc / hipHostRegister, e.g.
+ * kmws_host_alloc) that the loop reads sockets into: chunks fed from inside it
+ * are not copied -- their masked payloads are unmasked in place there
+ * (zero-copy), and the callback views point into the ring.  The ring bytes of a
+ * frame must stay unmodified until the frame is delivered.  Only while the
+ * batch holds no frames; NULL detaches. */
 kmws_status    kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes);
 void           kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec);
 
@@ -166,13 +180,18 @@ void           kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec);
  * :390/:415, then encodeFrameHeader) and the payload segments are queued for
  * masking with hdr->maskey when hdr->mask is set and the payload is not empty
  * (kuma's client mode: mask = 1 and a fresh key per frame, :386/:411; keys are
- * inputs here) -- and kmws_tx_batch_flush masks every queued payload in place
- * with one GPU launch, key phase continuing across a frame's segments.  The
- * segments must stay valid and unmodified until the flush; the iovec list for
- * the socket is then [hdr_out, segments...] as in :419-431.  A send with more
- * than 128 non-empty segments returns KMWS_ERR_BUFFER_TOO_LONG, and -- as in
- * kuma, which masks before counting iovecs -- its payload is still masked at
- * the flush.  Payloads over 4 GiB - 1 are refused (KMWS_ERR_INVALID_PARAM). */
+ * inputs here) -- and masks every queued payload in place with one GPU launch,
+ * key phase continuing across a frame's segments: kmws_tx_batch_flush
+ * (synchronous), or kmws_tx_batch_submit (returns a ticket at once) and
+ * kmws_tx_batch_poll(ticket) (1 once every generation up to the ticket is
+ * masked and back in the caller's buffers, 0 while in flight; wait != 0
+ * blocks), so the loop fills and submits the next iteration's sends while
+ * this one's masks run.  The segments must stay valid and unmodified until
+ * their generation completed; the iovec list for the socket is then [hdr_out,
+ * segments...] as in :419-431.  A send with more than 128 non-empty segments
+ * returns KMWS_ERR_BUFFER_TOO_LONG, and -- as in kuma, which masks before
+ * counting iovecs -- its payload is still masked.  Payloads over 4 GiB - 1
+ * are refused (KMWS_ERR_INVALID_PARAM). */
 typedef struct kmws_tx_batch kmws_tx_batch;
 kmws_tx_batch* kmws_tx_batch_create(int device);      /* NULL without a gfx950 device */
 void           kmws_tx_batch_destroy(kmws_tx_batch* b);
@@ -182,11 +201,15 @@ int            kmws_tx_batch_add(kmws_tx_batch* b, const kmws_frame_hdr* hdr, ui
 /* Masks every queued payload (one launch, synchronous); returns the number of
  * frames masked, or a negative kmws_status.  The batch is empty afterwards. */
 int64_t        kmws_tx_batch_flush(kmws_tx_batch* b);
+/* Enqueues the mask of every queued payload; returns its ticket (> 0), 0 if
+ * nothing was queued, or a negative kmws_status. */
+int64_t        kmws_tx_batch_submit(kmws_tx_batch* b);
+int            kmws_tx_batch_poll(kmws_tx_batch* b, int64_t ticket, int wait);
 int            kmws_tx_batch_pending(const kmws_tx_batch* b);
 /* Optional pinned send ring (hipHostMalloc / hipHostRegister) the loop builds
- * its outgoing payloads in: segments inside it are masked in place there at
- * flush (zero-copy, one launch), the others go through pinned staging.  Only
- * while the batch is empty; NULL detaches. */
+ * its outgoing payloads in: segments inside it are masked in place there
+ * (zero-copy, one launch), the others go through pinned staging.  Only while
+ * no sends are queued; NULL detaches. */
 kmws_status    kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ring_bytes);
 
 /* ======================= device batch entries ======================= */
@@ -218,39 +241,37 @@ kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, 
 kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                               const void* workspace, size_t workspace_bytes, void* stream);
 
-/* Optional one-time tuning (like a cuDNN benchmark pass): runs each unmask
- * schedule -- one block per tile, a persistent grid-stride grid, or a
- * software-pipelined persistent grid -- twice
- * on this batch (the XOR applied twice leaves the payload unchanged), times
- * them with events on `stream` (synchronizes) and makes the fastest the
- * current device's schedule for kmws_unmask_apply / kmws_unmask_batch.
- * Returns the chosen schedule or a negative status, one block per 16 KiB tile:
- * the XCDs in 2 groups, each dealing runs of 16 tiles inside its own half of
- * the span (0, the default), in order (1), tiles dealt over 2 (2), 8 (3) or 4 (5)
- * far-apart parts of the span, runs of 16 tiles per XCD (4); >= 64: a
- * persistent grid of that many blocks (+1: the pipelined grid); codes 0, 2-5 with bit 30 set
- * (KMWS_SCHED_TEMPORAL_STORES): the same split grids storing the payload with temporal stores
- * (the autotune times every one of them that way too).  kmws_unmask_schedule() reports the current one. */
+/* Unmask schedules.  The apply grid is one block per 16 KiB tile; a schedule
+ * says which tiles the resident blocks stream at once and how the payload is
+ * stored.  Placement kind (low byte): */
+#define KMWS_SCHED_GROUPED_RUNS 0   /* XCDs in 2 groups, runs of 16 tiles in each group's half (default) */
+#define KMWS_SCHED_IN_ORDER     1   /* tile = block */
+#define KMWS_SCHED_SPLIT2       2   /* blocks dealt over 2 far-apart parts of the span */
+#define KMWS_SCHED_SPLIT8       3   /* ... over 8 parts */
+#define KMWS_SCHED_XCD_RUNS     4   /* runs of 16 tiles per XCD */
+#define KMWS_SCHED_SPLIT4       5   /* ... over 4 parts */
+/* Store policy (at most one bit; neither = automatic: temporal stores when every
+ * frame of the batch starts on a 16 KiB tile boundary -- the plan records the
+ * layout -- non-temporal otherwise, e.g. for a packed wire image). */
+#define KMWS_SCHED_NT_STORES       (1 << 29)
 #define KMWS_SCHED_TEMPORAL_STORES (1 << 30)
+
+/* Optional one-time tuning of ONE batch (like a cuDNN benchmark pass): runs
+ * every placement kind with both store policies twice on this batch (the XOR
+ * applied twice leaves the payload unchanged), times them with events on
+ * `stream` (synchronizes) and records the fastest for this batch -- the tuple
+ * (workspace, descs, n, span) -- where kmws_unmask_apply / kmws_unmask_batch
+ * find it.  Every other batch keeps the default schedule (grouped runs,
+ * automatic stores): no device-global state.  Returns the chosen schedule code
+ * or a negative status. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
-int kmws_unmask_schedule(void);
-/* Tuning info: blocks of the persistent unmask kernel resident at once on the
- * current device (CUs x blocks per CU), or 0 on failure. */
-int kmws_unmask_resident_blocks(void);
-
-/* Tuning variant of kmws_unmask_batch: tile 16 KiB (0), 32 KiB (1), 64 KiB (2);
- * 16 KiB tiles on a persistent grid-stride grid of 8 K (3), 16 K (4), 24 K (5),
- * 32 K (6) or 64 K (7) blocks; one block per tile with registers capped for 6 (8)
- * or 8 (9) waves per SIMD; pipelined persistent grid of 16 K (10), 32 K (11) or
- * 64 K (12) blocks; one block per 16 KiB tile dealt over 2, 4, 8, 16 (21-24) or
- * 3, 6, 12, 32 (30-33) parts of the span, or in runs of 4, 8, 16, 32, 128 tiles
- * over the 8 XCDs (25-29); 32 KiB tiles over 2 / 8 parts (34, 35); runs of 16
- * tiles per XCD with the XCDs in 2 / 4 / 8 groups, each group in its own part of
- * the span (36-38); any value >= 64: a schedule code as kmws_unmask_schedule()
- * returns. */
-kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                      void* workspace, size_t workspace_bytes, void* stream, int variant);
+/* Pin a schedule for one batch (e.g. one measured offline), or forget it
+ * (schedule < 0: back to the default).  One entry per workspace. */
+kmws_status kmws_unmask_set_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span,
+                                     int schedule);
+/* The schedule code kmws_unmask_apply uses for this batch. */
+int kmws_unmask_get_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span);
 
 /* Read (synchronously) the status word of a workspace after a batch call:
  * 0 = OK, 1 = descriptor precondition violated, 2 = header error seen. */
@@ -365,52 +386,13 @@ kmws_status kmws_pipeline_set_transfer(kmws_pipeline* p, int mode);
 kmws_status kmws_pipeline_unmask(kmws_pipeline* p, uint8_t* host_base, uint64_t span, const kmws_desc* descs,
                                  uint32_t n);
 
-/* ---- payload arenas ---- */
-
-/* Device memory for a batch arena, physically contiguous when the device can
- * provide it (hipExtMallocWithFlags + hipDeviceMallocContiguous), else a plain
- * hipMalloc.  Where an allocation lands in HBM decides how well the unmask
- * schedule spreads its in-flight windows over the memory: contiguous arenas
- * held 81-83 % of peak, plain 64 GiB allocations 76-83 % depending on the
- * allocation.  *contiguous (optional) reports which one was
- * obtained.  Free with kmws_arena_free.  Returns NULL on failure. */
-void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous);
-void  kmws_arena_free(void* p, int device);
+/* ---- pinned host memory for the loop rings ---- */
 
 /* Page-locked host memory for the receive / send rings (kmws_rx_batch_attach_ring,
  * kmws_tx_batch_attach_ring): hipHostMalloc'ed, visible to `device`, so a
  * caller like kuma needs no HIP headers of its own.  NULL on failure. */
 void* kmws_host_alloc(size_t bytes, int device);
 void  kmws_host_free(void* p);
-
-/* Placement probe for a long-lived batch region inside an arena: times in-place
- * split-4 and split-8 unmasks of `span` bytes (uniform 64 KiB probe frames, each
- * applied twice, so the arena's bytes are unchanged) at offsets 0, step, 2*step,
- * ... (offset + span <= arena_bytes) and returns the byte offset where the better
- * of the two is fastest, or a negative kmws_status.  The split schedules run 76 % or 82-85 % of HBM
- * peak depending on where the batch lies in physical HBM, which the kernel
- * cannot see (DESIGN.md sec.4 "Placement").  frac_out (optional, max_out
- * entries) receives each offset's rate as a fraction of 8 TB/s.  A setup call:
- * allocates its probe descriptors and workspace, synchronizes the stream. */
-int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, uint64_t step, void* stream,
-                         float* frac_out, uint32_t max_out);
-
-/* ---- synthetic data + checks (bench / test support, device side) ---- */
-
-/* base[i] for i < bytes := byte (i & 7) of splitmix64(seed + (i >> 3)). */
-kmws_status kmws_fill_synthetic(uint8_t* base, uint64_t bytes, uint64_t seed, void* stream);
-
-/* Uniform descriptors: desc i = {i*stride, len, key_i}, key_i = low 32 bits of
- * splitmix64(key_seed + i). */
-kmws_status kmws_fill_uniform_descs(kmws_desc* descs, uint32_t n, uint64_t stride, uint32_t len,
-                                    uint64_t key_seed, void* stream);
-
-/* Independent byte-wise checker: counts bytes of base[0..bytes) that differ
- * from synthetic(seed) XOR (the key byte of the covering frame, if any) into
- * *mismatches (device u64, accumulated).  Descriptors must be sorted. */
-kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t seed,
-                                const kmws_desc* descs, uint32_t n,
-                                unsigned long long* mismatches, void* stream);
 
 #ifdef __cplusplus
 }

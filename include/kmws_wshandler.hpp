@@ -36,6 +36,18 @@
 //  * self-destruction from inside the frame callback (the reference's
 //    DestroyDetector, WSHandler.cpp:284-287) is supported: the decoder state
 //    is reference-counted and outlives the feed that is delivering.
+//
+// Batched mode (RxLoop below): kuma calls handleData once per 64 KiB socket
+// read; a GPU round trip per read costs about what the CPU's whole unmask of
+// the read does.  With an RxLoop attached (one per event-loop thread), handleData
+// parses and validates at once -- same return values -- and queues the frames
+// on the loop's receive batch; the loop's posted task (kuma: EventLoop::post,
+// kmapi.h:204-210) submits ONE GPU unmask for everything queued in the
+// iteration and delivers the callbacks of finished generations at the next
+// iterations, so the GPU round trip overlaps the loop's socket reads.  A CLOSE
+// frame or a decode error makes handleData deliver everything queued before it
+// returns, so kuma's onWsData (WebSocketImpl.cpp:225-246) sees the same state
+// and return value as with the reference.
 #ifndef KMWS_WSHANDLER_HPP
 #define KMWS_WSHANDLER_HPP
 
@@ -51,6 +63,86 @@
 
 namespace kmws {
 
+// The deferred receive batch of one event-loop thread, shared by every handler
+// on that loop, and the once-per-iteration hook that runs it.
+class RxLoop {
+public:
+    using Task = std::function<void()>;
+    using Poster = std::function<void(Task)>;  // kuma: [loop](Task t) { loop->post(std::move(t)); }
+
+    // async: submit at the end of an iteration, deliver at the next ones (the
+    // default); false: one synchronous flush per iteration.
+    explicit RxLoop(Poster post, int device = 0, bool async = true)
+        : post_(std::move(post)), batch_(kmws_rx_batch_create(device)), async_(async), alive_(std::make_shared<bool>(true))
+    {
+    }
+    ~RxLoop()
+    {
+        *alive_ = false;  // a posted task still queued on the loop becomes a no-op
+        if (batch_) {
+            (void)kmws_rx_batch_flush(batch_);
+            kmws_rx_batch_destroy(batch_);
+        }
+    }
+    RxLoop(const RxLoop&) = delete;
+    RxLoop& operator=(const RxLoop&) = delete;
+
+    // The RxLoop of the calling (event-loop) thread, created on first use.
+    static RxLoop& forThisThread(Poster post, int device = 0)
+    {
+        thread_local RxLoop loop(std::move(post), device);
+        return loop;
+    }
+
+    bool valid() const { return batch_ != nullptr; }
+    kmws_rx_batch* batch() const { return batch_; }
+
+    // Pinned receive ring the loop reads sockets into (kmws_host_alloc): payloads
+    // lying in it are unmasked there, without copies.  Ring bytes of a frame
+    // must stay unmodified until it was delivered (inflight() == 0 frees all).
+    int attachRing(uint8_t* ring, size_t bytes) { return kmws_rx_batch_attach_ring(batch_, ring, bytes); }
+
+    // Called after every deferred feed: posts the iteration's task once.
+    void arm()
+    {
+        if (armed_ || !post_) return;
+        armed_ = true;
+        std::weak_ptr<bool> alive = alive_;
+        post_([this, alive] {
+            std::shared_ptr<bool> a = alive.lock();
+            if (a && *a) runIteration();
+        });
+    }
+
+    // The posted task: submit what the iteration fed, deliver what finished;
+    // re-arms itself while generations are in flight.
+    void runIteration()
+    {
+        armed_ = false;
+        if (!async_) {
+            last_ = kmws_rx_batch_flush(batch_);
+            return;
+        }
+        const int s = kmws_rx_batch_submit(batch_);
+        last_ = s < 0 ? s : kmws_rx_batch_poll(batch_, 0);
+        if (kmws_rx_batch_inflight(batch_) > 0 || kmws_rx_batch_pending(batch_) > 0) arm();
+    }
+
+    // Deliver everything queued and in flight now (synchronous).
+    int flush() { return last_ = kmws_rx_batch_flush(batch_); }
+    int inflight() const { return kmws_rx_batch_inflight(batch_); }
+    int pending() const { return kmws_rx_batch_pending(batch_); }
+    int lastResult() const { return last_; }  // frames delivered by the last run, or a kmws_status
+
+private:
+    Poster post_;
+    kmws_rx_batch* batch_;
+    bool async_;
+    bool armed_ = false;
+    int last_ = 0;
+    std::shared_ptr<bool> alive_;
+};
+
 template <class FrameHeader, class Buffer, class WSError, class WSMode, class CbResult>
 class BasicWSHandler {
 public:
@@ -59,7 +151,10 @@ public:
     explicit BasicWSHandler(int device = 0) : st_(std::make_shared<State>(device)) {}
     ~BasicWSHandler()
     {
-        if (st_) st_->alive = false;  // a feed in progress keeps the state until it returns
+        if (st_) {
+            st_->alive = false;  // a feed in progress keeps the state until it returns
+            if (st_->rx && st_->dec) kmws_rx_batch_discard(st_->rx->batch(), st_->dec);  // queued frames: dropped
+        }
     }
     BasicWSHandler(const BasicWSHandler&) = delete;
     BasicWSHandler& operator=(const BasicWSHandler&) = delete;
@@ -81,12 +176,19 @@ public:
     {
         std::shared_ptr<State> keep = st_;
         if (!keep->dec) return WSError::INVALID_STATE;
+        if (keep->rx) return handleDeferred(keep, data, len);
         const int r = kmws_decoder_feed(keep->dec, data, len, &State::on_frame, keep.get());
         if (!keep->alive) return WSError::DESTROYED;
         keep->last_status = r < 0 ? r : KMWS_OK;
         if (r < 0) return WSError::INVALID_STATE;  // device step failed: lastStatus() says why
         return static_cast<WSError>(r);
     }
+
+    // Batched mode: queue decoded frames on the loop's receive batch (see the
+    // file comment).  nullptr returns to one GPU batch per handleData.  Switch
+    // only while none of this handler's frames are queued.
+    void setRxLoop(RxLoop* loop) { st_->rx = loop && loop->valid() ? loop : nullptr; }
+    RxLoop* rxLoop() const { return st_->rx; }
 
     // kmws_status of the last handleData: KMWS_OK, or why the GPU step failed
     int lastStatus() const { return st_->last_status; }
@@ -131,18 +233,46 @@ public:
     {
         std::vector<uint8_t*> segs;
         std::vector<size_t> lens;
+        collectSegments(buf, segs, lens);
+        if (segs.empty()) return KMWS_OK;
+        return kmws_mask_host_chain(mask_key, segs.data(), lens.data(), segs.size(), device);
+    }
+
+    // The chain's segments in order (KMBuffer::begin/end, kmbuffer.h:706-772), as
+    // handleDataMask hands them to kmws_mask_host_chain.
+    static void collectSegments(const Buffer& buf, std::vector<uint8_t*>& segs, std::vector<size_t>& lens)
+    {
         for (auto it = buf.begin(); it != buf.end(); ++it) {
             segs.push_back(static_cast<uint8_t*>(it->readPtr()));
             lens.push_back(it->length());
         }
-        if (segs.empty()) return KMWS_OK;
-        return kmws_mask_host_chain(mask_key, segs.data(), lens.data(), segs.size(), device);
     }
 
     static bool isControlFrame(uint8_t opcode) { return opcode >= 8; }  // WSHandler.h:52-54
 
 private:
-    struct State {
+    struct State;
+
+    static WSError handleDeferred(const std::shared_ptr<State>& keep, uint8_t* data, size_t len)
+    {
+        RxLoop* rx = keep->rx;
+        const int r = kmws_decoder_feed_deferred(keep->dec, rx->batch(), data, len, &State::on_frame, keep.get());
+        if (r == KMWS_WS_NOERR || r == KMWS_WS_NEED_MORE_DATA) {
+            rx->arm();
+            keep->last_status = KMWS_OK;
+            return static_cast<WSError>(r);
+        }
+        // CLOSE or an error: deliver everything queued first, so the caller sees
+        // the connection state the reference's synchronous delivery leaves
+        // (kuma's onWsData checks it before the return value)
+        const int f = rx->flush();
+        if (!keep->alive) return WSError::DESTROYED;
+        keep->last_status = r < 0 ? r : (f < 0 ? f : KMWS_OK);
+        if (r < 0) return WSError::INVALID_STATE;
+        return static_cast<WSError>(r);
+    }
+
+    struct State : std::enable_shared_from_this<State> {
         explicit State(int device) : dec(kmws_decoder_create(KMWS_MODE_CLIENT, device)) {}
         ~State()
         {
@@ -156,7 +286,9 @@ private:
         // the handler
         static int on_frame(const kmws_frame_hdr* k, uint8_t* payload, size_t len, void* user)
         {
-            State* s = static_cast<State*>(user);
+            // held for the call: the callback may destroy the handler (deferred
+            // delivery runs outside handleData, with no caller holding the state)
+            std::shared_ptr<State> s = static_cast<State*>(user)->shared_from_this();
             FrameHeader h;
             std::memset(static_cast<void*>(&h), 0, sizeof(h));
             h.fin = k->fin;
@@ -182,6 +314,7 @@ private:
         WSMode mode = WSMode::CLIENT;
         bool alive = true;
         int last_status = KMWS_OK;
+        RxLoop* rx = nullptr;
     };
     std::shared_ptr<State> st_;
 };

@@ -16,6 +16,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <new>
 #include <vector>
 
@@ -76,21 +78,42 @@ struct kmws_decoder {
 
 struct kmws_rx_batch {
     struct Item {
-        kmws_decoder* dec;  // identity only; never dereferenced at flush
+        kmws_decoder* dec;  // identity only; never dereferenced at delivery
         kmws_frame_cb cb;
         void* user;
         kmws_frame_hdr hdr;
-        size_t off;       // payload offset in the staging area (direct == nullptr)
+        size_t off;       // payload offset in the generation's staging area (direct == nullptr)
         uint8_t* direct;  // payload in the attached ring (no copy)
         bool live;        // false once discarded
     };
-    PinnedStage stage;
+    // One submitted generation: its frames, and the pinned stage that holds
+    // their staged payloads and the unmask launch in flight.
+    struct Gen {
+        std::unique_ptr<PinnedStage> stage;
+        std::vector<Item> items;
+    };
+    std::unique_ptr<PinnedStage> stage;  // the generation being fed
     std::vector<Item> items;
+    std::vector<kmws_desc> ring_descs;
+    std::deque<Gen> inflight;            // submitted, not yet delivered (submit order)
+    std::vector<std::unique_ptr<PinnedStage>> spare;
+    std::vector<Item>* delivering = nullptr;  // the generation whose callbacks are running
     uint8_t* ring = nullptr;  // caller's pinned receive ring (optional)
     size_t ring_bytes = 0;
-    std::vector<kmws_desc> ring_descs;
     int device = 0;
-    bool flushing = false;  // feeding the batch from inside its own flush is refused
+    bool flushing = false;  // feeding / submitting / polling from inside a delivery is refused
+
+    std::unique_ptr<PinnedStage> take_stage()
+    {
+        if (!spare.empty()) {
+            std::unique_ptr<PinnedStage> s = std::move(spare.back());
+            spare.pop_back();
+            return s;
+        }
+        std::unique_ptr<PinnedStage> s(new (std::nothrow) PinnedStage());
+        if (s && s->init(device) != KMWS_OK) s.reset();
+        return s;
+    }
 };
 
 namespace {
@@ -448,6 +471,13 @@ void kmws_host_free(void* p)
 }
 
 // ---- batched send path (SURVEY f-2) ----
+//
+// Sends queued with kmws_tx_batch_add form the current generation;
+// kmws_tx_batch_submit enqueues ONE mask launch for it and returns a ticket;
+// kmws_tx_batch_poll(ticket) completes generations up to the ticket (staged
+// segments are copied back into the caller's buffers) -- the loop writes a
+// generation's iovecs once its ticket completed, and can fill and submit the
+// next generation meanwhile.  kmws_tx_batch_flush = submit + poll(wait).
 
 struct kmws_tx_batch {
     struct Seg {
@@ -459,7 +489,13 @@ struct kmws_tx_batch {
         size_t bytes;
         uint32_t key;
     };
-    PinnedStage stage;
+    struct Gen {  // submitted: the stage with the launch in flight, segments to copy back
+        std::unique_ptr<PinnedStage> stage;
+        std::vector<Seg> segs;
+        std::vector<size_t> offs;  // staging offset per segment (SIZE_MAX: masked in the ring)
+        int64_t ticket;
+    };
+    std::unique_ptr<PinnedStage> stage;
     std::vector<Seg> segs;
     std::vector<Frame> frames;
     size_t bytes = 0;
@@ -467,9 +503,23 @@ struct kmws_tx_batch {
     uint8_t* ring = nullptr;  // caller's pinned send ring (optional)
     size_t ring_bytes = 0;
     std::vector<kmws_desc> ring_descs;
+    std::deque<Gen> inflight;
+    std::vector<std::unique_ptr<PinnedStage>> spare;
+    int64_t next_ticket = 1, done_ticket = 0;
     bool in_ring(const uint8_t* p, size_t n) const
     {
         return ring && p >= ring && n <= ring_bytes && (size_t)(p - ring) <= ring_bytes - n;
+    }
+    std::unique_ptr<PinnedStage> take_stage()
+    {
+        if (!spare.empty()) {
+            std::unique_ptr<PinnedStage> s = std::move(spare.back());
+            spare.pop_back();
+            return s;
+        }
+        std::unique_ptr<PinnedStage> s(new (std::nothrow) PinnedStage());
+        if (s && s->init(device) != KMWS_OK) s.reset();
+        return s;
     }
 };
 
@@ -478,14 +528,20 @@ kmws_tx_batch* kmws_tx_batch_create(int device)
     kmws_tx_batch* b = new (std::nothrow) kmws_tx_batch();
     if (!b) return nullptr;
     b->device = device;
-    if (b->stage.init(device) != KMWS_OK) {
+    b->stage = b->take_stage();
+    if (!b->stage) {
         delete b;
         return nullptr;
     }
     return b;
 }
 
-void kmws_tx_batch_destroy(kmws_tx_batch* b) { delete b; }
+void kmws_tx_batch_destroy(kmws_tx_batch* b)
+{
+    if (!b) return;
+    for (auto& g : b->inflight) (void)g.stage->wait();  // no launch may outlive its pinned memory
+    delete b;
+}
 
 int kmws_tx_batch_pending(const kmws_tx_batch* b) { return b ? (int)b->frames.size() : 0; }
 
@@ -533,13 +589,15 @@ kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ri
 // One descriptor per segment, its key rotated by the frame bytes before it
 // (the phase continues across segments, WSHandler.cpp:312-322): segments in
 // the attached pinned ring are masked in place there, the others gathered
-// into pinned staging and scattered back; one launch per buffer.
-int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
+// into pinned staging and copied back when the generation completes; one
+// launch per buffer.
+int64_t kmws_tx_batch_submit(kmws_tx_batch* b)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
-    const int64_t nf = (int64_t)b->frames.size();
-    if (nf == 0) return 0;
-    PinnedStage& s = b->stage;
+    if (b->frames.empty()) return 0;
+    std::unique_ptr<PinnedStage> next = b->take_stage();
+    if (!next) return KMWS_ERR_FAILED;
+    PinnedStage& s = *b->stage;
     s.clear();
     b->ring_descs.clear();
     size_t staged = 0;
@@ -563,34 +621,91 @@ int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
                 phase += g.len;
             }
         }
-        st = b->ring_descs.empty() ? s.run() : s.run(b->ring, b->ring_bytes, &b->ring_descs);
+        st = b->ring_descs.empty() ? s.launch() : s.launch(b->ring, b->ring_bytes, &b->ring_descs);
     }
-    if (st == KMWS_OK)
-        for (size_t i = 0; i < b->segs.size(); ++i)
-            if (offs[i] != SIZE_MAX) std::memcpy(b->segs[i].p, s.data() + offs[i], b->segs[i].len);
-    s.clear();
     b->frames.clear();
-    b->segs.clear();
     b->ring_descs.clear();
     b->bytes = 0;
-    return st == KMWS_OK ? nf : (int64_t)st;
+    if (st != KMWS_OK) {
+        b->segs.clear();
+        s.clear();
+        b->spare.push_back(std::move(next));
+        return st;
+    }
+    kmws_tx_batch::Gen g;
+    g.stage = std::move(b->stage);
+    g.segs.swap(b->segs);
+    g.offs.swap(offs);
+    g.ticket = b->next_ticket++;
+    b->inflight.push_back(std::move(g));
+    b->stage = std::move(next);
+    return b->inflight.back().ticket;
+}
+
+int kmws_tx_batch_poll(kmws_tx_batch* b, int64_t ticket, int wait)
+{
+    if (!b || ticket < 0) return KMWS_ERR_INVALID_PARAM;
+    kmws_status err = KMWS_OK;
+    while (!b->inflight.empty() && b->inflight.front().ticket <= ticket) {
+        kmws_tx_batch::Gen& g = b->inflight.front();
+        if (!wait && !g.stage->done()) break;
+        const kmws_status st = g.stage->wait();
+        if (st == KMWS_OK) {
+            for (size_t i = 0; i < g.segs.size(); ++i)
+                if (g.offs[i] != SIZE_MAX) std::memcpy(g.segs[i].p, g.stage->data() + g.offs[i], g.segs[i].len);
+        } else {
+            err = st;
+        }
+        b->done_ticket = g.ticket;
+        g.stage->clear();
+        b->spare.push_back(std::move(g.stage));
+        b->inflight.pop_front();
+    }
+    if (err != KMWS_OK) return err;
+    return ticket <= b->done_ticket || b->inflight.empty() || b->inflight.front().ticket > ticket ? 1 : 0;
+}
+
+int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
+{
+    if (!b) return KMWS_ERR_INVALID_PARAM;
+    const int64_t nf = (int64_t)b->frames.size();
+    const int64_t t = kmws_tx_batch_submit(b);
+    if (t < 0) return t;
+    const int r = kmws_tx_batch_poll(b, b->next_ticket - 1, 1);
+    if (r < 0) return r;
+    return nf;
 }
 
 // ---- deferred delivery across calls and connections ----
+//
+// Frames fed with kmws_decoder_feed_deferred collect in the batch's current
+// generation (payloads copied into its pinned stage, or left where they lie in
+// the attached ring).  kmws_rx_batch_submit enqueues ONE unmask launch for the
+// generation and returns at once; kmws_rx_batch_poll delivers the callbacks of
+// every generation whose launch has finished, in submit order (wait != 0: all
+// of them).  kmws_rx_batch_flush = submit + poll(wait).  So an event loop can
+// submit at the end of an iteration and deliver at the next one: the GPU round
+// trip overlaps the loop's socket reads instead of stalling them.
 
 kmws_rx_batch* kmws_rx_batch_create(int device)
 {
     kmws_rx_batch* b = new (std::nothrow) kmws_rx_batch();
     if (!b) return nullptr;
     b->device = device;
-    if (b->stage.init(device) != KMWS_OK) {
+    b->stage = b->take_stage();
+    if (!b->stage) {
         delete b;
         return nullptr;
     }
     return b;
 }
 
-void kmws_rx_batch_destroy(kmws_rx_batch* b) { delete b; }
+void kmws_rx_batch_destroy(kmws_rx_batch* b)
+{
+    if (!b) return;
+    for (auto& g : b->inflight) (void)g.stage->wait();  // no launch may outlive its pinned memory
+    delete b;
+}
 
 int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_t* data, size_t len,
                                kmws_frame_cb cb, void* user)
@@ -598,22 +713,22 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
     if (!dec || !b || (len && !data)) return KMWS_ERR_INVALID_PARAM;
     if (b->flushing) return KMWS_ERR_INVALID_STATE;
     // The chunk does not outlive this call (kuma reads into a stack buffer,
-    // TcpConnection.cpp:229), so every payload is copied into the batch.  The
-    // parse does not write into the chunk.
+    // TcpConnection.cpp:229), so every payload is copied into the batch unless
+    // it lies in the attached ring.  The parse does not write into the chunk.
     auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>* reasm) -> int {
         uint32_t key;
         std::memcpy(&key, h.maskey, 4);
         const bool masked = h.mask && h.length;
         if (!reasm && b->ring && payload >= b->ring && payload + h.length <= b->ring + b->ring_bytes) {
-            // payload lies in the caller's pinned ring: unmasked there at flush, no copy
+            // payload lies in the caller's pinned ring: unmasked there, no copy
             if (masked) b->ring_descs.push_back(kmws_desc{(uint64_t)(payload - b->ring), h.length, key});
             b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, 0, payload, true});
             return KMWS_OK;
         }
-        kmws_status st = b->stage.reserve(h.length);
+        kmws_status st = b->stage->reserve(h.length);
         if (st != KMWS_OK) return st;
-        const size_t off = b->stage.append(payload, h.length);
-        if (masked) b->stage.add_desc(off, h.length, key);
+        const size_t off = b->stage->append(payload, h.length);
+        if (masked) b->stage->add_desc(off, h.length, key);
         b->items.push_back(kmws_rx_batch::Item{dec, cb, user, h, off, nullptr, true});
         return KMWS_OK;
     };
@@ -622,7 +737,7 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
 
 kmws_status kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes)
 {
-    if (!b || b->flushing || !b->items.empty()) return KMWS_ERR_INVALID_STATE;
+    if (!b || b->flushing || !b->items.empty() || !b->inflight.empty()) return KMWS_ERR_INVALID_STATE;
     if (ring && (!bytes || !device_view(ring))) return KMWS_ERR_INVALID_PARAM;  // must be pinned
     b->ring = ring;
     b->ring_bytes = ring ? bytes : 0;
@@ -631,37 +746,91 @@ kmws_status kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t by
 
 int kmws_rx_batch_pending(const kmws_rx_batch* b) { return b ? (int)b->items.size() : 0; }
 
+int kmws_rx_batch_inflight(const kmws_rx_batch* b) { return b ? (int)b->inflight.size() : 0; }
+
 void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
 {
     if (!b) return;
     for (auto& it : b->items)
         if (it.dec == dec) it.live = false;
+    for (auto& g : b->inflight)
+        for (auto& it : g.items)
+            if (it.dec == dec) it.live = false;
+    if (b->delivering)
+        for (auto& it : *b->delivering)
+            if (it.dec == dec) it.live = false;
+}
+
+int kmws_rx_batch_submit(kmws_rx_batch* b)
+{
+    if (!b) return KMWS_ERR_INVALID_PARAM;
+    if (b->flushing) return KMWS_ERR_INVALID_STATE;
+    if (b->items.empty()) return 0;
+    std::unique_ptr<PinnedStage> next = b->take_stage();
+    if (!next) return KMWS_ERR_FAILED;
+    kmws_status st = b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs);
+    b->ring_descs.clear();
+    if (st != KMWS_OK) {
+        // nothing of this generation can be delivered masked: drop it
+        b->items.clear();
+        b->stage->clear();
+        b->spare.push_back(std::move(next));
+        return st;
+    }
+    const int n = (int)b->items.size();
+    kmws_rx_batch::Gen g;
+    g.stage = std::move(b->stage);
+    g.items.swap(b->items);
+    b->inflight.push_back(std::move(g));
+    b->stage = std::move(next);
+    return n;
+}
+
+int kmws_rx_batch_poll(kmws_rx_batch* b, int wait)
+{
+    if (!b) return KMWS_ERR_INVALID_PARAM;
+    if (b->flushing) return KMWS_ERR_INVALID_STATE;
+    int delivered = 0;
+    kmws_status err = KMWS_OK;
+    while (!b->inflight.empty()) {
+        kmws_rx_batch::Gen& g = b->inflight.front();
+        if (!wait && !g.stage->done()) break;
+        const kmws_status st = g.stage->wait();
+        std::vector<kmws_rx_batch::Item> items;
+        items.swap(g.items);
+        std::unique_ptr<PinnedStage> stage = std::move(g.stage);
+        b->inflight.pop_front();
+        if (st != KMWS_OK) {  // the launch failed: these payloads are still masked, never delivered
+            err = st;
+            stage->clear();
+            b->spare.push_back(std::move(stage));
+            continue;
+        }
+        std::vector<const kmws_decoder*> destroyed;
+        b->flushing = true;
+        b->delivering = &items;
+        for (auto& it : items) {
+            if (!it.live) continue;
+            bool dead = false;
+            for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
+            if (dead) continue;
+            ++delivered;  // a NULL callback consumes the frame, like WSHandler without frame_cb_ (:286)
+            uint8_t* payload = it.direct ? it.direct : stage->data() + it.off;
+            if (it.cb && it.cb(&it.hdr, payload, it.hdr.length, it.user)) destroyed.push_back(it.dec);
+        }
+        b->delivering = nullptr;
+        b->flushing = false;
+        stage->clear();
+        b->spare.push_back(std::move(stage));
+    }
+    return err != KMWS_OK ? err : delivered;
 }
 
 int kmws_rx_batch_flush(kmws_rx_batch* b)
 {
-    if (!b) return KMWS_ERR_INVALID_PARAM;
-    if (b->flushing) return KMWS_ERR_INVALID_STATE;
-    kmws_status st = b->stage.run(b->ring, b->ring_bytes, &b->ring_descs);
-    if (st != KMWS_OK) return st;
-    std::vector<kmws_rx_batch::Item> items;
-    items.swap(b->items);
-    int delivered = 0;
-    std::vector<const kmws_decoder*> destroyed;
-    b->flushing = true;
-    for (auto& it : items) {
-        if (!it.live) continue;
-        bool dead = false;
-        for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
-        if (dead) continue;
-        ++delivered;  // a NULL callback consumes the frame, like WSHandler without frame_cb_ (:286)
-        uint8_t* payload = it.direct ? it.direct : b->stage.data() + it.off;
-        if (it.cb && it.cb(&it.hdr, payload, it.hdr.length, it.user)) destroyed.push_back(it.dec);
-    }
-    b->flushing = false;
-    b->stage.clear();
-    b->ring_descs.clear();
-    return delivered;
+    const int s = kmws_rx_batch_submit(b);
+    const int d = kmws_rx_batch_poll(b, 1);
+    return s < 0 ? s : d;
 }
 
 }  // extern "C"

@@ -54,10 +54,12 @@ inline size_t grow(size_t need, size_t have)
 }
 
 // A batch of payloads unmasked in place by the GPU.  Payloads are appended to
-// a pinned host area (16-B aligned starts); run() launches the pieces kernel
-// on the pinned area itself (zero-copy over PCIe) and waits.
-// An optional second batch of descriptors can target another pinned buffer
-// (a caller's registered receive buffer).
+// a pinned host area (16-B aligned starts); launch() enqueues the pieces kernel
+// on the pinned area itself (zero-copy over PCIe) on the stage's own stream and
+// records its completion event; run() = launch() + wait.  An optional second
+// batch of descriptors can target another pinned buffer (a caller's registered
+// receive or send ring).  The asynchronous rx / tx batches keep one stage per
+// generation in flight (kmws_decoder.cpp).
 class PinnedStage {
 public:
     ~PinnedStage() { release(); }
@@ -72,6 +74,7 @@ public:
         if (!stream_) {
             DevGuard g(device_);
             if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return KMWS_ERR_FAILED;
+            if (hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess) return KMWS_ERR_FAILED;
         }
         return KMWS_OK;
     }
@@ -126,6 +129,31 @@ public:
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                     const std::vector<kmws_desc>* extra = nullptr)
     {
+        kmws_status st = launch(extra_base, extra_span, extra);
+        if (st != KMWS_OK) return st;
+        return wait();
+    }
+
+    // Has the last launch() finished?  (true when nothing was launched)
+    bool done() const
+    {
+        if (!launched_) return true;
+        const hipError_t e = hipEventQuery(done_);
+        if (e == hipErrorNotReady) return false;
+        (void)hipGetLastError();
+        return true;  // finished, or failed: wait() reports which
+    }
+    kmws_status wait()
+    {
+        if (!launched_) return KMWS_OK;
+        launched_ = false;
+        return hipEventSynchronize(done_) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
+    }
+
+    // Enqueue the unmask of every staged descriptor (and `extra`) without waiting.
+    kmws_status launch(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
+                       const std::vector<kmws_desc>* extra = nullptr)
+    {
         const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
         if (n1 + n2 == 0) return KMWS_OK;
         DevGuard g(device_);
@@ -166,7 +194,9 @@ public:
             st = launch_unmask_pieces(dv, dv_desc_ + n1, dv_piece_ + p1, (uint32_t)p2, stream_);
             if (st != KMWS_OK) return st;
         }
-        return hipStreamSynchronize(stream_) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
+        if (hipEventRecord(done_, stream_) != hipSuccess) return KMWS_ERR_FAILED;
+        launched_ = true;
+        return KMWS_OK;
     }
 
 private:
@@ -204,6 +234,7 @@ private:
     void release()
     {
         if (stream_) (void)hipStreamSynchronize(stream_);
+        if (done_) (void)hipEventDestroy(done_);
         if (h_) (void)hipHostFree(h_);
         if (h_desc_) (void)hipHostFree(h_desc_);
         if (h_piece_) (void)hipHostFree(h_piece_);
@@ -213,6 +244,8 @@ private:
     int device_ = 0;
     int dev_ok_ = -1;
     hipStream_t stream_ = nullptr;
+    hipEvent_t done_ = nullptr;
+    bool launched_ = false;
     uint8_t* h_ = nullptr;
     uint8_t* dv_h_ = nullptr;
     size_t cap_ = 0, len_ = 0;

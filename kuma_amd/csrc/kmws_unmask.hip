@@ -14,8 +14,11 @@
 // mask (a rotated key splatted over the payload bytes of the word; header or
 // gap bytes get 0), XORs and stores whole 16-byte words.  HBM-bound: 2 bytes
 // of traffic per payload byte + 16 B per descriptor; no MFMA.
-#include "kmws_common.hpp"
+#include <atomic>
+#include <mutex>
 
+#include "kmws_bench.h"
+#include "kmws_common.hpp"
 
 // Uncapped split grids (batches of frames shorter than a tile, the LDS-staged
 // path) load the tile's descriptors before its payload: cfg4's in-place unmask
@@ -49,26 +52,33 @@ struct UnmaskCfg {
 
 // Tile -> first frame map.  Frame f owns tile starts in [start_f, next_f)
 // where start_0 = 0, start_f = off_f, next_f = off_{f+1} (span for the last).
-// Validates sortedness / non-overlap / bounds on the fly.
+// Validates sortedness / non-overlap / bounds on the fly, and records in the
+// workspace head whether any frame starts off a tile boundary (the layout the
+// automatic store policy of the apply grid reads).
 __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __restrict__ d, uint32_t n,
                                                           uint64_t span, uint32_t tile_shift,
                                                           uint32_t* __restrict__ map,
                                                           WsHead* __restrict__ head)
 {
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    if (f >= n) return;
-    const kmws_desc df = d[f];
-    const uint64_t next = (f + 1 < n) ? d[f + 1].off : span;
-    if (df.off > span || df.off + (uint64_t)df.len > next) {
-        atomicOr(&head->status, kStatusBadDesc);
-        return;
-    }
-    const uint64_t start = f == 0 ? 0 : df.off;
     const uint64_t T = 1ull << tile_shift;
-    const uint64_t b0 = (start + T - 1) >> tile_shift;
-    const uint64_t b1 = (next + T - 1) >> tile_shift;
-    for (uint64_t b = b0; b < b1; ++b) map[b] = f;
-    if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
+    bool unaligned = false;
+    if (f < n) {
+        const kmws_desc df = d[f];
+        const uint64_t next = (f + 1 < n) ? d[f + 1].off : span;
+        unaligned = (df.off & (T - 1)) != 0;
+        if (df.off > span || df.off + (uint64_t)df.len > next) {
+            atomicOr(&head->status, kStatusBadDesc);
+        } else {
+            const uint64_t start = f == 0 ? 0 : df.off;
+            const uint64_t b0 = (start + T - 1) >> tile_shift;
+            const uint64_t b1 = (next + T - 1) >> tile_shift;
+            for (uint64_t b = b0; b < b1; ++b) map[b] = f;
+            if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
+        }
+    }
+    // one atomic per block at most (a packed wire sets it from every block)
+    if (__syncthreads_or(unaligned) && threadIdx.x == 0) atomicOr(&head->layout, kLayoutUnaligned);
 }
 
 // Issue every payload load of a tile.  Full tiles load unconditionally so the
@@ -230,49 +240,51 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
     }
 }
 
-// One block per tile.  W = minimum waves per SIMD the register allocation must
-// allow (1 = unconstrained; the tuning variants test 6 and 8).
-template <int V, int W = 1, bool TWO = false>
-__global__ void __launch_bounds__(kBlock, W) unmask_tiles_kernel(uint8_t* __restrict__ base, uint64_t span,
-                                                              const kmws_desc* __restrict__ d, uint32_t n,
-                                                              const uint32_t* __restrict__ map,
-                                                              const WsHead* __restrict__ head, uint32_t tile_base)
+// Payload store policy of an apply grid (the schedule's store bits): automatic
+// = temporal when every frame of the batch starts on a tile boundary (the plan's
+// layout flag, read after the payload loads), non-temporal otherwise; or forced.
+enum StorePolicy : uint32_t { kStoreAuto = 0, kStoreNT = 1, kStoreTemporal = 2 };
+
+__device__ __forceinline__ bool nt_stores(const WsHead* head, uint32_t store)
+{
+    return store == kStoreNT || (store == kStoreAuto && (head->layout & kLayoutUnaligned) != 0);
+}
+
+// One block for the partial last tile of a span (the split grids take the full
+// tiles).  Metadata comes after the payload loads, with no early exit between
+// the loads and their uses, so the compiler cannot sink the loads below the
+// scalar metadata waits.  A bad plan (status != 0) stores nothing.
+template <int V>
+__global__ void __launch_bounds__(kBlock) unmask_tail_kernel(uint8_t* __restrict__ base, uint64_t span,
+                                                             const kmws_desc* __restrict__ d, uint32_t n,
+                                                             const uint32_t* __restrict__ map,
+                                                             const WsHead* __restrict__ head, uint32_t tile)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
     __shared__ uint64_t s_end[Cfg::kCap];
     __shared__ uint32_t s_key[Cfg::kCap];
-    const uint32_t tile = tile_base + blockIdx.x;
     const uint64_t tile_lo = (uint64_t)tile * Cfg::kTile;
     u32x4 v[V];
-    // Metadata comes after the payload loads, with no early exit between the
-    // loads and their uses, so the compiler cannot sink the loads below the
-    // scalar metadata waits.  A bad plan (status != 0) stores nothing.
-    if (tile_lo + Cfg::kTile <= span) {
-        load_tile<V, true>(base, tile_lo, tile_lo + Cfg::kTile, v);
-        __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true, TWO>(base, tile_lo, tile_lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off,
-                             s_end, s_key);
-    } else {
-        load_tile<V, false>(base, tile_lo, span, v);
-        __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, false>(base, tile_lo, span, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
-    }
+    load_tile<V, false>(base, tile_lo, span, v);
+    __builtin_amdgcn_sched_barrier(0);
+    finish_tile<V, false>(base, tile_lo, span, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
 }
 
-// One block per full tile like unmask_tiles_kernel, blocks dealt over `k`
-// equal parts of the span: block b takes tile (b mod k) * (nfull / k) + b / k,
-// so the blocks in flight stream k windows far apart instead of one (the
-// blocks past k * (nfull / k) take the remaining tiles in order).  With c > 0
+// One block per full tile, blocks dealt over `k` equal parts of the span:
+// block b takes tile (b mod k) * (nfull / k) + b / k, so the blocks in flight
+// stream k windows far apart instead of one (the blocks past k * (nfull / k)
+// take the remaining tiles in order; k = 1 is the in-order grid).  With c > 0
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
-// its own runs).
-template <int V, bool TWO = false, bool NT = true>
+// its own runs).  `store`: StorePolicy.
+template <int V, bool TWO = false>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w)
+                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w,
+                                                              uint32_t store)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -311,87 +323,25 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
         if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
         load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
-                                      s_key, &pre);
+        const bool ok = head->status == 0;
+        if (nt_stores(head, store))
+            finish_tile<V, true, TWO, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key,
+                                            &pre);
+        else
+            finish_tile<V, true, TWO, false>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key,
+                                             &pre);
         return;
     }
 #endif
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
-                                  s_key);
-}
-
-// Grid-stride over the full tiles [0, nfull): block b takes tiles b, b+G, ...
-// and issues the next tile's loads before finishing the current one.
-template <int V>
-__global__ void __launch_bounds__(kBlock) unmask_persist_kernel(uint8_t* __restrict__ base,
-                                                                const kmws_desc* __restrict__ d, uint32_t n,
-                                                                const uint32_t* __restrict__ map,
-                                                                const WsHead* __restrict__ head, uint32_t nfull)
-{
-    using Cfg = UnmaskCfg<V>;
-    __shared__ uint64_t s_off[Cfg::kCap];
-    __shared__ uint64_t s_end[Cfg::kCap];
-    __shared__ uint32_t s_key[Cfg::kCap];
-    uint32_t t = blockIdx.x;
-    if (t >= nfull) return;
+    // the head (status, layout) is read after the payload loads: its latency
+    // hides under theirs, and the store policy is a block-uniform branch
     const bool ok = head->status == 0;
-    u32x4 v[V];
-    load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, v);
-    for (;;) {
-        const uint32_t tn = t + gridDim.x;
-        u32x4 w[V];
-        if (tn < nfull) load_tile<V, true>(base, (uint64_t)tn * Cfg::kTile, 0, w);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t lo = (uint64_t)t * Cfg::kTile;
-        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, t, ok, v, s_off, s_end, s_key);
-        if (tn >= nfull) break;
-#pragma unroll
-        for (int i = 0; i < V; ++i) v[i] = w[i];
-        t = tn;
-    }
-}
-
-// Grid-stride like unmask_persist_kernel, software-pipelined for real: two
-// register sets used in turn (a copy from one to the other waits for the loads
-// in flight), and a loop with one exit at the bottom -- both steps run every
-// trip, a step past the end loads a clamped tile and stores nothing -- so the
-// wait before a tile's stores counts only that tile's loads.
-template <int V>
-__global__ void __launch_bounds__(kBlock) unmask_pipe_kernel(uint8_t* __restrict__ base,
-                                                             const kmws_desc* __restrict__ d, uint32_t n,
-                                                             const uint32_t* __restrict__ map,
-                                                             const WsHead* __restrict__ head, uint32_t nfull)
-{
-    using Cfg = UnmaskCfg<V>;
-    __shared__ uint64_t s_off[Cfg::kCap];
-    __shared__ uint64_t s_end[Cfg::kCap];
-    __shared__ uint32_t s_key[Cfg::kCap];
-    uint32_t t = blockIdx.x;
-    if (t >= nfull) return;
-    const bool ok = head->status == 0;
-    const uint32_t last = nfull - 1;
-    u32x4 va[V], vb[V];
-    load_tile<V, true>(base, (uint64_t)t * Cfg::kTile, 0, va);
-    auto step = [&](const u32x4(&vc)[V], u32x4(&vn)[V]) __attribute__((always_inline)) {
-        const uint32_t tn = t + gridDim.x;
-        const bool more = tn < nfull;
-        load_tile<V, true>(base, (uint64_t)(more ? tn : last) * Cfg::kTile, 0, vn);
-        __builtin_amdgcn_sched_barrier(0);
-        const bool live = t < nfull;
-        const uint32_t tt = live ? t : last;
-        const uint64_t lo = (uint64_t)tt * Cfg::kTile;
-        finish_tile<V, true>(base, lo, lo + Cfg::kTile, d, n, map, tt, ok && live, vc, s_off, s_end, s_key);
-        __builtin_amdgcn_sched_barrier(0);
-        t = tn;
-        return more;
-    };
-    for (;;) {
-        const bool a = step(va, vb);
-        const bool b = step(vb, va);
-        if (!(a & b)) break;
-    }
+    if (nt_stores(head, store))
+        finish_tile<V, true, TWO, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key);
+    else
+        finish_tile<V, true, TWO, false>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key);
 }
 
 // Small host batches: the decoder's payloads of one socket read or one loop
@@ -509,18 +459,6 @@ __global__ void __launch_bounds__(kBlock) check_unmasked_kernel(const uint8_t* _
 
 // Tile geometry used by the product path (tuned on MI355X).
 constexpr int kUnmaskV = 4;
-
-// Apply schedule per device (codes: launch_schedule).  Where the blocks in
-// flight are decides the rate: the in-order grid streams one 16 MiB window
-// (74.5-75 % of HBM peak everywhere); dealing blocks over 8 parts of the span
-// streams 8 windows far apart (82-83 % on some 64 GiB placements in HBM, 76 %
-// on others); runs of 16 tiles per XCD hold 78-79 % on every placement; two
-// groups of 4 XCDs, each with runs of 16 in its own half of the span, match
-// the better of the two on every placement measured and lead on 4 KiB frames
-// (82 %) (profiles/r01f_unmask_placement.txt).  Default: the grouped runs;
-// kmws_unmask_autotune picks per device on the caller's batch.
-constexpr int kMaxDevices = 64;
-static uint32_t g_schedule[kMaxDevices];
 using ProdCfg = UnmaskCfg<kUnmaskV>;
 
 // Blocks of an apply grid resident per CU.  Fewer blocks in flight stream HBM
@@ -528,11 +466,33 @@ using ProdCfg = UnmaskCfg<kUnmaskV>;
 // the 64 GiB batch at 84.5-84.8 % of peak against 82.4-82.9 % with the 6 the
 // registers allow, 3 blocks at 83.4 %, 1 block at 65-75 %
 // (profiles/r02ag_unmask_occupancy.txt).  The cap is dynamic LDS the kernel does
-// not use: a block asks for just over a third of the CU's LDS.
-// KMWS_UNMASK_BLOCKS_PER_CU overrides it for every batch (0 = no cap; tuning).
-constexpr uint32_t kUnmaskBlocksPerCU = 2;
-constexpr uint32_t kUnmaskStaticLds = UnmaskCfg<4>::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
-static unsigned unmask_lds_pad_device();
+// not use: a block asks for just over a third of the CU's LDS.  Compile-time
+// (a tuning build may define another value; 0 = no cap).
+#ifndef KMWS_UNMASK_BLOCKS_PER_CU
+#define KMWS_UNMASK_BLOCKS_PER_CU 2
+#endif
+constexpr uint32_t kUnmaskStaticLds = ProdCfg::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
+
+static unsigned unmask_lds_pad_device()
+{
+    static thread_local int dev_cached = -1;
+    static thread_local unsigned pad = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev != dev_cached) {
+        int lds = 0;
+        pad = 0;
+        if (KMWS_UNMASK_BLOCKS_PER_CU > 0 &&
+            hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) == hipSuccess &&
+            lds > 0) {
+            const unsigned per_block = (unsigned)lds / (unsigned)(KMWS_UNMASK_BLOCKS_PER_CU + 1) + 1;  // one more does not fit
+            pad = per_block > kUnmaskStaticLds ? per_block - kUnmaskStaticLds : 0u;
+        }
+        dev_cached = dev;
+    }
+    return pad;
+}
+
 // The cap pays where tiles take the one- or two-frame paths (regions of a tile
 // or more: 16 KiB frames ran 85.5 % capped vs 79-83 % uncapped); batches of
 // smaller frames (several per tile: the LDS-staged path, whose barriers need the
@@ -541,30 +501,7 @@ static unsigned unmask_lds_pad_device();
 // Mean region >= 1 tile selects.
 static unsigned unmask_lds_pad(uint64_t span, uint32_t n)
 {
-    static const bool forced = getenv("KMWS_UNMASK_BLOCKS_PER_CU") != nullptr;  // tuning: the cap on every batch
-    return forced || (n && span / n >= UnmaskCfg<4>::kTile) ? unmask_lds_pad_device() : 0u;
-}
-static unsigned unmask_lds_pad_device()
-{
-    static thread_local int dev_cached = -1;
-    static thread_local unsigned pad = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (dev != dev_cached) {
-        static const int want = [] {
-            const char* e = getenv("KMWS_UNMASK_BLOCKS_PER_CU");
-            return e ? atoi(e) : (int)kUnmaskBlocksPerCU;
-        }();
-        int lds = 0;
-        pad = 0;
-        if (want > 0 && hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) ==
-                            hipSuccess && lds > 0) {
-            const unsigned per_block = (unsigned)lds / (unsigned)(want + 1) + 1;  // want + 1 blocks do not fit
-            pad = per_block > kUnmaskStaticLds ? per_block - kUnmaskStaticLds : 0u;
-        }
-        dev_cached = dev;
-    }
-    return pad;
+    return n && span / n >= ProdCfg::kTile ? unmask_lds_pad_device() : 0u;
 }
 
 static uint32_t ilog2_u64(uint64_t x)
@@ -574,194 +511,158 @@ static uint32_t ilog2_u64(uint64_t x)
     return r;
 }
 
-template <int V>
 static kmws_status check_ws(uint64_t span, size_t ws_bytes, uint64_t* ntiles_out)
 {
-    using Cfg = UnmaskCfg<V>;
-    const uint64_t ntiles = (span + Cfg::kTile - 1) / Cfg::kTile;
+    const uint64_t ntiles = (span + ProdCfg::kTile - 1) / ProdCfg::kTile;
     if (ntiles > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
     if (ws_bytes < sizeof(WsHead) + (ntiles + 1) * sizeof(uint32_t)) return KMWS_ERR_BUFFER_TOO_SMALL;
     *ntiles_out = ntiles;
     return KMWS_OK;
 }
 
-template <int V>
-static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
-                               size_t ws_bytes, hipStream_t s)
+static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace, size_t ws_bytes,
+                               hipStream_t s)
 {
     uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    kmws_status st = check_ws(span, ws_bytes, &ntiles);
     if (st != KMWS_OK) return st;
     WsHead* head = static_cast<WsHead*>(workspace);
     if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     if (n == 0 || span == 0) return KMWS_OK;
     hipLaunchKernelGGL(tile_map_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, n, span,
-                       ilog2_u64(UnmaskCfg<V>::kTile), reinterpret_cast<uint32_t*>(head + 1), head);
+                       ilog2_u64(ProdCfg::kTile), reinterpret_cast<uint32_t*>(head + 1), head);
     return hip_status(hipGetLastError());
 }
 
-template <int V, int W = 1>
-static kmws_status launch_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+// ---- schedules: where the blocks in flight are, and the store policy ----
+//
+// The tile kernel is the same for every schedule; what differs is which tiles
+// the ~512 resident blocks stream at once (the in-order grid streams one 16 MiB
+// window: 74.5-75 % of HBM peak everywhere; dealing blocks over far-apart parts
+// of the span streams several windows: 82-86 % on some placements in physical
+// HBM, 76 % on others; runs of 16 tiles per XCD hold 78-79 % on every placement;
+// profiles/r01f_unmask_placement.txt, r02al_unmask_schedules_2bpc.txt) and how the
+// payload is stored (temporal stores gain 0.3-1 point on tile-aligned batches and
+// lose 1.6-7 on packed wire images, r02bz_unmask_store_policy_ab.txt).
+//
+// A schedule belongs to ONE batch: kmws_unmask_autotune / kmws_unmask_set_schedule
+// record it for (workspace, descs, n, span), and apply uses it only for that
+// batch; every other batch gets the default (grouped XCD runs, automatic store
+// policy).  The reference's handleDataMask (WSHandler.cpp:303-310) is stateless;
+// so is every batch that was not tuned.
+struct Split {
+    uint32_t k, c, w;
+};
+constexpr uint32_t kKindMask = 0xFFu;
+constexpr uint32_t kSchedTemporal = KMWS_SCHED_TEMPORAL_STORES;
+constexpr uint32_t kSchedNT = KMWS_SCHED_NT_STORES;
+constexpr uint32_t kDefaultSchedule = KMWS_SCHED_GROUPED_RUNS;
+
+static bool split_of(uint32_t kind, Split* sp)
+{
+    switch (kind) {
+    case KMWS_SCHED_GROUPED_RUNS: *sp = {8u, 16u, 2u}; return true;  // 2 groups of 4 XCDs, runs of 16 per half
+    case KMWS_SCHED_IN_ORDER: *sp = {1u, 0u, 1u}; return true;
+    case KMWS_SCHED_SPLIT2: *sp = {2u, 0u, 1u}; return true;
+    case KMWS_SCHED_SPLIT8: *sp = {8u, 0u, 1u}; return true;
+    case KMWS_SCHED_XCD_RUNS: *sp = {8u, 16u, 1u}; return true;
+    case KMWS_SCHED_SPLIT4: *sp = {4u, 0u, 1u}; return true;
+    default: return false;
+    }
+}
+
+static bool valid_schedule(uint32_t code)
+{
+    Split sp;
+    const uint32_t store = code & (kSchedTemporal | kSchedNT);
+    return split_of(code & kKindMask, &sp) && store != (kSchedTemporal | kSchedNT) &&
+           (code & ~(kKindMask | kSchedTemporal | kSchedNT)) == 0;
+}
+
+static uint32_t store_policy(uint32_t code)
+{
+    return (code & kSchedTemporal) ? kStoreTemporal : ((code & kSchedNT) ? kStoreNT : kStoreAuto);
+}
+
+struct TunedBatch {
+    const void* ws;
+    const void* descs;
+    uint64_t span;
+    uint32_t n;
+    uint32_t code;
+};
+constexpr int kTunedSlots = 64;
+static std::mutex g_tuned_mu;
+static TunedBatch g_tuned[kTunedSlots];
+static std::atomic<int> g_tuned_count{0};
+static int g_tuned_next = 0;
+
+static uint32_t batch_schedule(const void* ws, const kmws_desc* descs, uint32_t n, uint64_t span)
+{
+    if (g_tuned_count.load(std::memory_order_acquire) == 0) return kDefaultSchedule;
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    for (const TunedBatch& t : g_tuned)
+        if (t.ws == ws && t.descs == descs && t.n == n && t.span == span) return t.code;
+    return kDefaultSchedule;
+}
+
+// Records (or, code < 0, forgets) the schedule of one batch.  One entry per
+// workspace: a workspace serves one batch at a time.
+static void record_schedule(const void* ws, const kmws_desc* descs, uint32_t n, uint64_t span, int64_t code)
+{
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    int slot = -1;
+    for (int i = 0; i < kTunedSlots; ++i)
+        if (g_tuned[i].ws == ws) slot = i;
+    if (code < 0) {
+        if (slot >= 0) {
+            g_tuned[slot] = TunedBatch{};
+            g_tuned_count.fetch_sub(1, std::memory_order_release);
+        }
+        return;
+    }
+    if (slot < 0) {
+        for (int i = 0; i < kTunedSlots && slot < 0; ++i)
+            if (!g_tuned[i].ws) slot = i;
+        if (slot < 0) {  // full: the oldest slot goes (a forgotten batch reverts to the default)
+            slot = g_tuned_next;
+            g_tuned_next = (g_tuned_next + 1) % kTunedSlots;
+        } else {
+            g_tuned_count.fetch_add(1, std::memory_order_release);
+        }
+    }
+    g_tuned[slot] = TunedBatch{ws, descs, span, n, (uint32_t)code};
+}
+
+static kmws_status launch_apply(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                 const void* workspace, size_t ws_bytes, hipStream_t s)
 {
+    Split sp;
+    if (!valid_schedule(code) || !split_of(code & kKindMask, &sp)) return KMWS_ERR_INVALID_PARAM;
     uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
-    if (st != KMWS_OK) return st;
-    if (n == 0 || span == 0) return KMWS_OK;
-    const WsHead* head = static_cast<const WsHead*>(workspace);
-    // A launch may hold at most 2^32 work-items: split huge spans into pieces.
-    constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
-    for (uint64_t t0 = 0; t0 < ntiles; t0 += kMaxBlocks) {
-        const uint64_t nb = ntiles - t0 < kMaxBlocks ? ntiles - t0 : kMaxBlocks;
-        const unsigned pad = unmask_lds_pad(span, n);
-        if (pad)
-            hipLaunchKernelGGL((unmask_tiles_kernel<V, W, true>), dim3((uint32_t)nb), dim3(kBlock), pad, s, base, span,
-                               descs, n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
-        else
-            hipLaunchKernelGGL((unmask_tiles_kernel<V, W>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, span, descs,
-                               n, reinterpret_cast<const uint32_t*>(head + 1), head, (uint32_t)t0);
-    }
-    return hip_status(hipGetLastError());
-}
-
-template <int V>
-static kmws_status launch_apply_persist(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                        const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t grid)
-{
-    using Cfg = UnmaskCfg<V>;
-    uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
+    kmws_status st = check_ws(span, ws_bytes, &ntiles);
     if (st != KMWS_OK) return st;
     if (n == 0 || span == 0) return KMWS_OK;
     const WsHead* head = static_cast<const WsHead*>(workspace);
     const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
-    const uint64_t nfull = span / Cfg::kTile;
-    if (nfull > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
-    if (nfull) {
-        const uint32_t g = (uint32_t)(nfull < grid ? nfull : grid);
-        hipLaunchKernelGGL(unmask_persist_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
-                           (uint32_t)nfull);
-    }
-    if (ntiles > nfull)  // the partial last tile
-        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
-                           (uint32_t)nfull);
-    return hip_status(hipGetLastError());
-}
-
-template <int V>
-static kmws_status launch_apply_pipe(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                     const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t grid)
-{
-    using Cfg = UnmaskCfg<V>;
-    uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
-    if (st != KMWS_OK) return st;
-    if (n == 0 || span == 0) return KMWS_OK;
-    const WsHead* head = static_cast<const WsHead*>(workspace);
-    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
-    const uint64_t nfull = span / Cfg::kTile;
-    if (nfull > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
-    if (nfull) {
-        const uint32_t g = (uint32_t)(nfull < grid ? nfull : grid);
-        hipLaunchKernelGGL(unmask_pipe_kernel<V>, dim3(g), dim3(kBlock), 0, s, base, descs, n, map, head,
-                           (uint32_t)nfull);
-    }
-    if (ntiles > nfull)  // the partial last tile
-        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
-                           (uint32_t)nfull);
-    return hip_status(hipGetLastError());
-}
-
-// Resident blocks of a kernel on the current device (CUs x blocks per CU).
-static uint32_t resident_blocks(const void* kernel)
-{
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess) return 0;
-    return (uint32_t)(cus * per);
-}
-
-template <int V, bool NT = true>
-static kmws_status launch_apply_split(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                      const void* workspace, size_t ws_bytes, hipStream_t s, uint32_t k,
-                                      uint32_t c = 0, uint32_t w = 1)
-{
-    using Cfg = UnmaskCfg<V>;
-    uint64_t ntiles = 0;
-    kmws_status st = check_ws<V>(span, ws_bytes, &ntiles);
-    if (st != KMWS_OK) return st;
-    if (n == 0 || span == 0) return KMWS_OK;
-    const WsHead* head = static_cast<const WsHead*>(workspace);
-    const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
-    const uint64_t nfull = span / Cfg::kTile;
-    if (nfull > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    const uint64_t nfull = span / ProdCfg::kTile;
+    const uint32_t store = store_policy(code);
     // a launch may hold at most 2^32 work-items: huge spans go in pieces of blocks
     constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
     const unsigned lds_pad = unmask_lds_pad(span, n);
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
         const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
         if (lds_pad)
-            hipLaunchKernelGGL((unmask_split_kernel<V, true, NT>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s, base,
-                               descs, n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, true>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s,
+                               base, descs, n, map, head, (uint32_t)nfull, sp.k, sp.c, (uint32_t)b0, sp.w, store);
         else
-            hipLaunchKernelGGL((unmask_split_kernel<V, false, NT>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base, descs,
-                               n, map, head, (uint32_t)nfull, k, c, (uint32_t)b0, w);
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, false>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base,
+                               descs, n, map, head, (uint32_t)nfull, sp.k, sp.c, (uint32_t)b0, sp.w, store);
     }
     if (ntiles > nfull)  // the partial last tile
-        hipLaunchKernelGGL(unmask_tiles_kernel<V>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
+        hipLaunchKernelGGL(unmask_tail_kernel<kUnmaskV>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
                            (uint32_t)nfull);
     return hip_status(hipGetLastError());
-}
-
-template <int V>
-static kmws_status launch_unmask(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                 void* workspace, size_t ws_bytes, hipStream_t s)
-{
-    kmws_status st = launch_plan<V>(span, descs, n, workspace, ws_bytes, s);
-    if (st != KMWS_OK) return st;
-    return launch_apply<V>(base, span, descs, n, workspace, ws_bytes, s);
-}
-
-// Flag on schedule codes 0, 2, 3, 4, 5: payload stores temporal instead of
-// non-temporal (store_word).
-constexpr uint32_t kSchedTemporal = 1u << 30;
-
-// Schedule code, one block per 16 KiB tile: the XCDs in 2 groups of 4, each
-// group dealing runs of 16 tiles to its XCDs inside its own half of the span
-// (0, the default), in order (1), tiles dealt over 2 parts of the span (2) or
-// over 8 parts (3), runs of 16 tiles per XCD in one window (4); codes >= 64: a
-// persistent grid of that many blocks, grid-stride (even) or software-pipelined
-// (odd, grid = code - 1).
-static kmws_status launch_schedule(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                   const void* workspace, size_t ws_bytes, hipStream_t s)
-{
-    if (code & kSchedTemporal) {  // the same split schedules with temporal payload stores
-        switch (code & ~kSchedTemporal) {
-        case 0: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u, 2u);
-        case 2: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 2u);
-        case 3: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u);
-        case 4: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
-        case 5: return launch_apply_split<kUnmaskV, false>(base, span, descs, n, workspace, ws_bytes, s, 4u);
-        default: return KMWS_ERR_INVALID_PARAM;
-        }
-    }
-    if (code == 0) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u, 2u);
-    if (code == 4) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u, 16u);
-    if (code == 1) return launch_apply<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s);
-    if (code == 2) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 2u);
-    if (code == 3) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 8u);
-    if (code == 5) return launch_apply_split<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, 4u);
-    if (code < 64) return KMWS_ERR_INVALID_PARAM;
-    if (code & 1u) return launch_apply_pipe<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code & ~1u);
-    return launch_apply_persist<kUnmaskV>(base, span, descs, n, workspace, ws_bytes, s, code);
-}
-
-static uint32_t current_schedule()
-{
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
-    return __atomic_load_n(&g_schedule[dev], __ATOMIC_RELAXED);
 }
 
 static bool bad_args(const uint8_t* base, const kmws_desc* descs, uint32_t n, const void* ws)
@@ -797,8 +698,7 @@ extern "C" {
 
 size_t kmws_unmask_workspace_size(uint64_t span)
 {
-    // sized for the smallest tile any variant uses (8 KiB: variants 40, 41)
-    const uint64_t ntiles = (span + UnmaskCfg<2>::kTile - 1) / UnmaskCfg<2>::kTile;
+    const uint64_t ntiles = (span + ProdCfg::kTile - 1) / ProdCfg::kTile;
     return sizeof(WsHead) + (size_t)(ntiles + 1) * sizeof(uint32_t);  // + the map's sentinel
 }
 
@@ -806,7 +706,7 @@ kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* des
                               void* workspace, size_t workspace_bytes, void* stream)
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+    kmws_status st = launch_plan(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
     if (st != KMWS_OK) return st;
     return kmws_unmask_apply(base, span, descs, n, workspace, workspace_bytes, stream);
 }
@@ -815,45 +715,45 @@ kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, 
                              size_t workspace_bytes, void* stream)
 {
     if (!workspace || (n && !descs)) return KMWS_ERR_INVALID_PARAM;
-    return launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
+    return launch_plan(span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
 kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                               const void* workspace, size_t workspace_bytes, void* stream)
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    return launch_schedule(current_schedule(), base, span, descs, n, workspace, workspace_bytes, s);
+    return launch_apply(batch_schedule(workspace, descs, n, span), base, span, descs, n, workspace, workspace_bytes,
+                        static_cast<hipStream_t>(stream));
 }
 
-int kmws_unmask_schedule(void) { return (int)current_schedule(); }
-
-int kmws_unmask_resident_blocks(void)
+int kmws_unmask_get_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span)
 {
-    return (int)resident_blocks(reinterpret_cast<const void*>(kmws::unmask_pipe_kernel<kUnmaskV>));
+    return (int)batch_schedule(workspace, descs, n, span);
+}
+
+kmws_status kmws_unmask_set_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span,
+                                     int schedule)
+{
+    if (!workspace) return KMWS_ERR_INVALID_PARAM;
+    if (schedule >= 0 && !valid_schedule((uint32_t)schedule)) return KMWS_ERR_INVALID_PARAM;
+    record_schedule(workspace, descs, n, span, schedule);
+    return KMWS_OK;
 }
 
 // Times each schedule on the caller's batch, twice per schedule (XOR applied
-// twice is the identity, so the payload is unchanged on return), and keeps the
-// fastest as this device's kmws_unmask_apply schedule.  Synchronizes.
+// twice is the identity, so the payload is unchanged on return), and records
+// the fastest for THIS batch (workspace, descs, n, span).  Synchronizes.
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream)
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return KMWS_ERR_FAILED;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    kmws_status st = launch_plan<kUnmaskV>(span, descs, n, workspace, workspace_bytes, s);
+    kmws_status st = launch_plan(span, descs, n, workspace, workspace_bytes, s);
     if (st != KMWS_OK) return st;
-    // grouped XCD runs, 4 parts, 8 parts, XCD runs, 2 parts, in order: which wins
-    // depends on where the batch lies in HBM, on its frame layout and on the
-    // blocks in flight (profiles/r01f_unmask_placement.txt; at 2 blocks per CU
-    // 4 parts led with 85.3 %, profiles/r02al_unmask_schedules_2bpc.txt)
-    // (+ the split schedules with temporal stores: faster on aligned arenas,
-    // slower on packed wire images, profiles/r02bz_unmask_store_policy_ab.txt;
-    // with them split 2 leads on the aligned arena, r02cj_unmask_ts_candidates_ab.txt)
-    static const uint32_t cand[] = {0u, 5u, 3u, 4u, 2u, 1u, 5u | kSchedTemporal, 3u | kSchedTemporal,
-                                    2u | kSchedTemporal, 0u | kSchedTemporal, 4u | kSchedTemporal};
+    // every placement kind x both store policies: which wins depends on where the
+    // batch lies in HBM, on its frame layout and on the blocks in flight
+    static const uint32_t kinds[] = {KMWS_SCHED_GROUPED_RUNS, KMWS_SCHED_SPLIT4, KMWS_SCHED_SPLIT8,
+                                     KMWS_SCHED_XCD_RUNS,     KMWS_SCHED_SPLIT2, KMWS_SCHED_IN_ORDER};
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return KMWS_ERR_FAILED;
     if (hipEventCreate(&e1) != hipSuccess) {
@@ -861,125 +761,33 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
         return KMWS_ERR_FAILED;
     }
     float best = 1e30f;
-    uint32_t pick = 0;
-    for (int rep = 0; rep < 2; ++rep) {
-        for (uint32_t g : cand) {
-            if (hipEventRecord(e0, s) != hipSuccess) { st = KMWS_ERR_FAILED; break; }
-            for (int k = 0; k < 2 && st == KMWS_OK; ++k)
-                st = launch_schedule(g, base, span, descs, n, workspace, workspace_bytes, s);
-            if (st != KMWS_OK || hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
-                st = st != KMWS_OK ? st : KMWS_ERR_FAILED;
-                break;
+    uint32_t pick = kDefaultSchedule;
+    for (int rep = 0; rep < 2 && st == KMWS_OK; ++rep) {
+        for (uint32_t kind : kinds) {
+            for (uint32_t store : {kSchedNT, kSchedTemporal}) {
+                const uint32_t g = kind | store;
+                if (hipEventRecord(e0, s) != hipSuccess) { st = KMWS_ERR_FAILED; break; }
+                for (int k = 0; k < 2 && st == KMWS_OK; ++k)
+                    st = launch_apply(g, base, span, descs, n, workspace, workspace_bytes, s);
+                if (st != KMWS_OK || hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) {
+                    st = st != KMWS_OK ? st : KMWS_ERR_FAILED;
+                    break;
+                }
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                if (rep == 1 && ms < best) {  // rep 0 warms every schedule up
+                    best = ms;
+                    pick = g;
+                }
             }
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, e0, e1);
-            if (rep == 1 && ms < best) {  // rep 0 warms every schedule up
-                best = ms;
-                pick = g;
-            }
+            if (st != KMWS_OK) break;
         }
-        if (st != KMWS_OK) break;
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (st != KMWS_OK) return st;
-    __atomic_store_n(&g_schedule[dev], pick, __ATOMIC_RELAXED);
+    record_schedule(workspace, descs, n, span, pick);
     return (int)pick;
-}
-
-// Tuning entry: same contract as kmws_unmask_batch with an explicit tile
-// variant (0: 16 KiB, 1: 32 KiB, 2: 64 KiB).  Used by bench/tune scripts.
-kmws_status kmws_unmask_batch_variant(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
-                                      void* workspace, size_t workspace_bytes, void* stream, int variant)
-{
-    if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    switch (variant) {
-    case 0: return launch_unmask<4>(base, span, descs, n, workspace, workspace_bytes, s);
-    case 1: return launch_unmask<8>(base, span, descs, n, workspace, workspace_bytes, s);
-    case 2: return launch_unmask<16>(base, span, descs, n, workspace, workspace_bytes, s);
-    case 3:
-    case 4:
-    case 5:
-    case 6:
-    case 7: {  // 16 KiB tiles, persistent grid-stride with next-tile prefetch: 4096 .. 16384 blocks
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t grids[] = {8192u, 16384u, 24576u, 32768u, 65536u};
-        const uint32_t grid = grids[variant - 3];
-        return launch_apply_persist<4>(base, span, descs, n, workspace, workspace_bytes, s, grid);
-    }
-    case 8:
-    case 9: {  // 16 KiB tiles, registers capped for 6 (8) or 8 (9) waves per SIMD
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return variant == 8 ? launch_apply<4, 6>(base, span, descs, n, workspace, workspace_bytes, s)
-                            : launch_apply<4, 8>(base, span, descs, n, workspace, workspace_bytes, s);
-    }
-    case 10:
-    case 11:
-    case 12: {  // 16 KiB tiles, pipelined persistent grid: 16384 / 32768 / 65536 blocks
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t grids[] = {16384u, 32768u, 65536u};
-        return launch_apply_pipe<4>(base, span, descs, n, workspace, workspace_bytes, s, grids[variant - 10]);
-    }
-    case 21:
-    case 22:
-    case 23:
-    case 24: {  // 16 KiB tiles, one block per tile, blocks dealt over 2 / 4 / 8 / 16 parts of the span
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 2u << (variant - 21));
-    }
-    case 25:
-    case 26:
-    case 27:
-    case 28:
-    case 29: {  // 16 KiB tiles, one block per tile, runs of 4 / 8 / 16 / 32 / 128 tiles per XCD residue
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t runs[] = {4u, 8u, 16u, 32u, 128u};
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, runs[variant - 25]);
-    }
-    case 30:
-    case 31:
-    case 32:
-    case 33: {  // 16 KiB tiles, one block per tile, blocks dealt over 3 / 6 / 12 / 32 parts of the span
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        static const uint32_t ks[] = {3u, 6u, 12u, 32u};
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, ks[variant - 30]);
-    }
-    case 34:
-    case 35: {  // 32 KiB tiles, one block per tile, blocks dealt over 2 / 8 parts of the span
-        kmws_status st = launch_plan<8>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return launch_apply_split<8>(base, span, descs, n, workspace, workspace_bytes, s, variant == 34 ? 2u : 8u);
-    }
-    case 36:
-    case 37:
-    case 38: {  // XCD runs of 16 tiles, the 8 residues in 2 / 4 / 8 groups, each group in its own window
-        kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return launch_apply_split<4>(base, span, descs, n, workspace, workspace_bytes, s, 8u, 16u,
-                                     2u << (variant - 36));
-    }
-    case 40:
-    case 41: {  // 8 KiB tiles, one block per tile: split 8 / XCD runs of 32 tiles
-        kmws_status st = launch_plan<2>(span, descs, n, workspace, workspace_bytes, s);
-        if (st != KMWS_OK) return st;
-        return variant == 40 ? launch_apply_split<2>(base, span, descs, n, workspace, workspace_bytes, s, 8u)
-                             : launch_apply_split<2>(base, span, descs, n, workspace, workspace_bytes, s, 8u, 32u);
-    }
-    default:
-        if (variant >= 64) {  // a raw schedule code (kmws_unmask_schedule's encoding)
-            kmws_status st = launch_plan<4>(span, descs, n, workspace, workspace_bytes, s);
-            if (st != KMWS_OK) return st;
-            return launch_schedule((uint32_t)variant, base, span, descs, n, workspace, workspace_bytes, s);
-        }
-        return KMWS_ERR_INVALID_PARAM;
-    }
 }
 
 kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream)
@@ -990,6 +798,20 @@ kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* 
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return hip_status(e);
 }
+
+int kmws_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    return good;
+}
+
+// ---------------- bench / test support (include/kmws_bench.h) ----------------
 
 void* kmws_arena_alloc(uint64_t bytes, int device, int* contiguous)
 {
@@ -1029,8 +851,8 @@ int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, ui
     // Offsets 0, step, 2 step, ... with offset + span <= arena_bytes.  The probe
     // batch: uniform 64 KiB frames over the span (contents are whatever the arena
     // holds; XOR applied twice leaves them unchanged); an offset scores the better
-    // of the split-4 and split-8 schedules (codes 5, 3: which one leads depends
-    // on the placement, and kmws_unmask_autotune then picks among all).
+    // of the split-4 and split-8 schedules (which one leads depends on the
+    // placement, and kmws_unmask_autotune then picks among all).
     constexpr uint64_t kFrame = 65536;
     if (!arena || span == 0 || span > arena_bytes || step == 0 || (step & 15u) ||
         (reinterpret_cast<uintptr_t>(arena) & 15u) || span / kFrame > 0xFFFFFFFFull)
@@ -1060,10 +882,11 @@ int64_t kmws_arena_place(uint8_t* arena, uint64_t arena_bytes, uint64_t span, ui
         for (uint64_t off = 0; st == KMWS_OK && off + span <= arena_bytes; off += step, ++k) {
             float t = 1e30f;
             for (int rep = 0; rep < 4 && st == KMWS_OK; ++rep) {  // min of two pairs per schedule
-                st = launch_plan<kUnmaskV>(span, d, n, ws, ws_bytes, s);
+                st = launch_plan(span, d, n, ws, ws_bytes, s);
                 if (st == KMWS_OK) st = hip_status(hipEventRecord(e0, s));
+                const uint32_t g = (rep & 1 ? KMWS_SCHED_SPLIT8 : KMWS_SCHED_SPLIT4) | kSchedNT;
                 for (int i = 0; i < 2 && st == KMWS_OK; ++i)
-                    st = launch_schedule(rep & 1 ? 3u : 5u, arena + off, span, d, n, ws, ws_bytes, s);
+                    st = launch_apply(g, arena + off, span, d, n, ws, ws_bytes, s);
                 if (st == KMWS_OK) st = hip_status(hipEventRecord(e1, s));
                 if (st == KMWS_OK) st = hip_status(hipEventSynchronize(e1));
                 float ms = 0;
@@ -1118,18 +941,6 @@ kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t se
     hipLaunchKernelGGL(check_unmasked_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                        base, bytes, seed, descs, n, mismatches);
     return hip_status(hipGetLastError());
-}
-
-int kmws_device_count(void)
-{
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-    int good = 0;
-    for (int i = 0; i < n; ++i) {
-        hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
-    }
-    return good;
 }
 
 }  // extern "C"

@@ -31,17 +31,28 @@ EXPORTS = [
     "kmws_encode_header", "kmws_header_size", "kmws_decoder_create", "kmws_decoder_destroy",
     "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
     "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
-    "kmws_unmask_batch_variant", "kmws_unmask_autotune", "kmws_unmask_schedule", "kmws_unmask_resident_blocks", "kmws_read_status", "kmws_fill_synthetic",
-    "kmws_fill_uniform_descs", "kmws_check_unmasked", "kmws_copy_workspace_size", "kmws_encode_batch",
+    "kmws_unmask_autotune", "kmws_unmask_set_schedule", "kmws_unmask_get_schedule", "kmws_read_status",
+    "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pack_headers_workspace_size", "kmws_pack_headers", "kmws_find_headers_streams",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
-    "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain",
-    "kmws_rx_batch_attach_ring", "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place",
+    "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain", "kmws_rx_batch_submit",
+    "kmws_rx_batch_poll", "kmws_rx_batch_inflight", "kmws_tx_batch_submit", "kmws_tx_batch_poll",
+    "kmws_rx_batch_attach_ring",
     "kmws_tx_batch_create", "kmws_tx_batch_destroy", "kmws_tx_batch_add", "kmws_tx_batch_flush",
     "kmws_tx_batch_pending", "kmws_tx_batch_attach_ring", "kmws_host_alloc", "kmws_host_free",
 ]
+#: every function include/kmws_bench.h declares (bench / test support, same library)
+BENCH_EXPORTS = [
+    "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
+    "kmws_check_unmasked",
+]
+
+# unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
+SCHED_GROUPED_RUNS, SCHED_IN_ORDER, SCHED_SPLIT2, SCHED_SPLIT8, SCHED_XCD_RUNS, SCHED_SPLIT4 = 0, 1, 2, 3, 4, 5
+SCHED_KINDS = (0, 1, 2, 3, 4, 5)
+SCHED_NT_STORES, SCHED_TEMPORAL_STORES = 1 << 29, 1 << 30
 
 
 class FrameHdr(C.Structure):
@@ -99,9 +110,8 @@ def lib() -> C.CDLL:
         "kmws_unmask_plan": (i32, [u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_apply": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_autotune": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
-        "kmws_unmask_schedule": (i32, []),
-        "kmws_unmask_resident_blocks": (i32, []),
-        "kmws_unmask_batch_variant": (i32, [u8p, u64, vp, u32, vp, sz, vp, i32]),
+        "kmws_unmask_set_schedule": (i32, [vp, vp, u32, u64, i32]),
+        "kmws_unmask_get_schedule": (i32, [vp, vp, u32, u64]),
         "kmws_read_status": (i32, [vp, C.POINTER(C.c_uint32), vp]),
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
         "kmws_arena_alloc": (vp, [u64, i32, C.POINTER(C.c_int)]),
@@ -125,6 +135,11 @@ def lib() -> C.CDLL:
         "kmws_tx_batch_destroy": (None, [vp]),
         "kmws_tx_batch_add": (i32, [vp, C.POINTER(FrameHdr), vp, vp, sz, vp]),
         "kmws_tx_batch_flush": (C.c_int64, [vp]),
+        "kmws_tx_batch_submit": (C.c_int64, [vp]),
+        "kmws_tx_batch_poll": (i32, [vp, C.c_int64, i32]),
+        "kmws_rx_batch_submit": (i32, [vp]),
+        "kmws_rx_batch_poll": (i32, [vp, i32]),
+        "kmws_rx_batch_inflight": (i32, [vp]),
         "kmws_tx_batch_pending": (i32, [vp]),
         "kmws_tx_batch_attach_ring": (i32, [vp, vp, sz]),
         "kmws_host_alloc": (vp, [sz, i32]),
@@ -152,6 +167,17 @@ class KmwsError(RuntimeError):
     def __init__(self, status: int, what: str):
         super().__init__(f"{what} failed with kmws_status {status}")
         self.status = status
+
+
+def _check_tensor(t, name: str, elem: int, device) -> None:
+    """Raw data_ptr() goes to the kernels: element size, layout and device must
+    match what the C ABI reads, or it would read past the tensor."""
+    if t.element_size() != elem:
+        raise TypeError(f"{name}: expected {elem}-byte elements, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
 
 
 def _check(st: int, what: str) -> None:
@@ -297,6 +323,23 @@ class RxBatch:
     def pending(self) -> int:
         return lib().kmws_rx_batch_pending(self._b)
 
+    def submit(self) -> int:
+        """kmws_rx_batch_submit: enqueue this generation's unmask, return at once."""
+        r = lib().kmws_rx_batch_submit(self._b)
+        if r < 0:
+            raise KmwsError(r, "kmws_rx_batch_submit")
+        return r
+
+    def poll(self, wait: bool = False) -> int:
+        """kmws_rx_batch_poll: deliver every finished generation (all with wait)."""
+        r = lib().kmws_rx_batch_poll(self._b, int(bool(wait)))
+        if r < 0:
+            raise KmwsError(r, "kmws_rx_batch_poll")
+        return r
+
+    def inflight(self) -> int:
+        return lib().kmws_rx_batch_inflight(self._b)
+
     def attach_ring(self, ring) -> None:
         """ring: pinned torch uint8 CPU tensor (kept alive by this object)."""
         self._ring = ring
@@ -350,6 +393,26 @@ class TxBatch:
 
     def pending(self) -> int:
         return lib().kmws_tx_batch_pending(self._b)
+
+    def submit(self) -> int:
+        """kmws_tx_batch_submit: enqueue the masks, return the generation's ticket."""
+        self._inflight = getattr(self, "_inflight", [])
+        t = lib().kmws_tx_batch_submit(self._b)
+        if t < 0:
+            raise KmwsError(t, "kmws_tx_batch_submit")
+        if t:
+            self._inflight.append((t, list(self._keep)))
+        self._keep.clear()
+        return t
+
+    def poll(self, ticket: int, wait: bool = False) -> bool:
+        """kmws_tx_batch_poll: True once every generation up to `ticket` is masked."""
+        r = lib().kmws_tx_batch_poll(self._b, ticket, int(bool(wait)))
+        if r < 0:
+            raise KmwsError(r, "kmws_tx_batch_poll")
+        if r:
+            self._inflight = [x for x in getattr(self, "_inflight", []) if x[0] > ticket]
+        return bool(r)
 
     def attach_ring(self, ring) -> None:
         """ring: pinned torch uint8 CPU tensor (kept alive by this object)."""
@@ -465,21 +528,19 @@ def unmask_workspace_size(span: int) -> int:
 
 
 def unmask_batch(base, descs, ws: Workspace, span: Optional[int] = None, stream=None,
-                 variant: Optional[int] = None) -> None:
-    """In-place batched unmask (kmws_unmask_batch) of uint8 device tensor `base`."""
+                 schedule: Optional[int] = None) -> None:
+    """In-place batched unmask (kmws_unmask_batch) of uint8 device tensor `base`.
+    `schedule` pins a schedule code for this batch first (kmws_unmask_set_schedule)."""
     span = base.numel() if span is None else span
     n = descs.shape[0]
-    s = _stream_handle(stream)
-    if variant is None:
-        st = lib().kmws_unmask_batch(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr, ws.nbytes, s)
-    else:
-        st = lib().kmws_unmask_batch_variant(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr,
-                                             ws.nbytes, s, variant)
-    _check(st, "kmws_unmask_batch")
+    if schedule is not None:
+        unmask_set_schedule(ws, descs, span, schedule)
+    _check(lib().kmws_unmask_batch(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr, ws.nbytes,
+                                   _stream_handle(stream)), "kmws_unmask_batch")
 
 
 def unmask_autotune(base, descs, ws: Workspace, span: Optional[int] = None, stream=None) -> int:
-    """kmws_unmask_autotune: pick this device's unmask schedule (payload unchanged)."""
+    """kmws_unmask_autotune: pick and record the schedule of THIS batch (payload unchanged)."""
     span = base.numel() if span is None else span
     r = lib().kmws_unmask_autotune(base.data_ptr(), span, descs.data_ptr(), descs.shape[0], ws.ptr, ws.nbytes,
                                    _stream_handle(stream))
@@ -488,12 +549,15 @@ def unmask_autotune(base, descs, ws: Workspace, span: Optional[int] = None, stre
     return r
 
 
-def unmask_schedule() -> int:
-    return lib().kmws_unmask_schedule()
+def unmask_set_schedule(ws: Workspace, descs, span: int, schedule: int) -> None:
+    """kmws_unmask_set_schedule: pin (schedule >= 0) or forget (< 0) this batch's schedule."""
+    _check(lib().kmws_unmask_set_schedule(ws.ptr, descs.data_ptr(), descs.shape[0], span, schedule),
+           "kmws_unmask_set_schedule")
 
 
-def unmask_resident_blocks() -> int:
-    return lib().kmws_unmask_resident_blocks()
+def unmask_get_schedule(ws: Workspace, descs, span: int) -> int:
+    """kmws_unmask_get_schedule: the schedule code apply uses for this batch."""
+    return lib().kmws_unmask_get_schedule(ws.ptr, descs.data_ptr(), descs.shape[0], span)
 
 
 def unmask_plan(descs, ws: Workspace, span: int, stream=None) -> None:
@@ -549,6 +613,13 @@ def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Wo
     """kmws_pack_headers: headers only, frame i's into the 16-B slot hdr[16 i:]
     (uint8 device tensor of >= 16 n bytes), lengths into hdr_len (uint8, n),
     wire offsets into wire_off (int64, n+1; needs ws)."""
+    _check_tensor(descs, "descs", 8, descs.device)
+    _check_tensor(flags, "flags", 2, descs.device)
+    _check_tensor(hdr, "hdr", 1, descs.device)
+    if hdr_len is not None:
+        _check_tensor(hdr_len, "hdr_len", 1, descs.device)
+    if wire_off is not None:
+        _check_tensor(wire_off, "wire_off", 8, descs.device)
     _check(lib().kmws_pack_headers(descs.data_ptr(), flags.data_ptr(), descs.shape[0], hdr.data_ptr(),
                                    hdr_len.data_ptr() if hdr_len is not None else None,
                                    wire_off.data_ptr() if wire_off is not None else None,
@@ -562,6 +633,9 @@ def find_headers_streams(wire, stream_off, cap: int, wire_len: Optional[int] = N
     Returns (hdr_off (n_streams, cap) int64 absolute offsets, n_out int32,
     consumed int64) device tensors."""
     import torch
+    _check_tensor(stream_off, "stream_off", 8, wire.device)
+    if stream_off.dtype != torch.int64:
+        raise TypeError("stream_off must be int64")
     ns = stream_off.shape[0] - 1
     wire_len = wire.numel() if wire_len is None else wire_len
     hdr = torch.empty((ns, max(cap, 1)), dtype=torch.int64, device=wire.device)

@@ -8,6 +8,8 @@
 //        wshandler_adapter nogpu    + masked paths must fail loudly (no device)
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -213,8 +215,151 @@ static void gpu_checks()
     }
 }
 
+// A minimal event loop: EventLoop::post appends a task, every iteration runs
+// the tasks queued before it (kmapi.h:204-210 "run the task at next time").
+struct FakeLoop {
+    std::deque<std::function<void()>> tasks;
+    kmws::RxLoop::Poster poster()
+    {
+        return [this](kmws::RxLoop::Task t) { tasks.push_back(std::move(t)); };
+    }
+    int iterate()
+    {
+        std::deque<std::function<void()>> now;
+        now.swap(tasks);
+        for (auto& t : now) t();
+        return (int)now.size();
+    }
+};
+
+static std::vector<uint8_t> masked_frame(int opcode, const std::string& payload, const uint8_t key[4], int fin = 1)
+{
+    std::vector<uint8_t> data(payload.begin(), payload.end());
+    FrameHeader h = make_hdr(fin, 0, opcode, 1, (uint32_t)data.size(), key);
+    uint8_t hb[14];
+    const int n = WSHandler::encodeFrameHeader(h, hb);
+    for (size_t i = 0; i < data.size(); ++i) data[i] ^= key[i % 4];
+    std::vector<uint8_t> w(hb, hb + n);
+    w.insert(w.end(), data.begin(), data.end());
+    return w;
+}
+
+// Batched mode: two connections on one loop, frames queued by handleData,
+// delivered by the loop's posted task (asynchronously: submit, then poll at
+// the next iterations), in order per connection; CLOSE and errors deliver
+// everything queued before handleData returns; a handler deleted by its own
+// callback during deferred delivery stops its delivery.
+static void batched_checks(bool async)
+{
+    FakeLoop loop;
+    kmws::RxLoop rx(loop.poster(), 0, async);
+    CHECK(rx.valid());
+    WSHandler a, b;
+    a.setMode(WSMode::SERVER);
+    b.setMode(WSMode::SERVER);
+    a.setRxLoop(&rx);
+    b.setRxLoop(&rx);
+    std::vector<Rec> ga, gb;
+    collect(a, ga);
+    collect(b, gb);
+    std::vector<std::string> sa, sb;
+    for (int it = 0; it < 6; ++it) {  // 6 loop iterations of reads on both connections
+        std::vector<uint8_t> wa, wb;
+        for (int j = 0; j < 3; ++j) {
+            const uint8_t key[4] = {(uint8_t)(it * 7 + j), 0x5a, (uint8_t)(j + 1), 0x0f};
+            std::string pa(100 + 517 * j + it, (char)('A' + (it + j) % 26));
+            std::string pb(3000 + j, (char)('a' + (it * 3 + j) % 26));
+            sa.push_back(pa);
+            sb.push_back(pb);
+            std::vector<uint8_t> fa = masked_frame(2, pa, key), fb = masked_frame(1, pb, key);
+            wa.insert(wa.end(), fa.begin(), fa.end());
+            wb.insert(wb.end(), fb.begin(), fb.end());
+        }
+        // reads cut mid-frame: the decoder reassembles across reads
+        const size_t cut = wa.size() / 2 + 3;
+        CHECK(a.handleData(wa.data(), cut) == WSError::NEED_MORE_DATA);
+        CHECK(b.handleData(wb.data(), wb.size()) == WSError::NOERR);
+        CHECK(a.handleData(wa.data() + cut, wa.size() - cut) == WSError::NOERR);
+        loop.iterate();
+    }
+    for (int spin = 0; spin < 100000 && (rx.inflight() || rx.pending() || !loop.tasks.empty()); ++spin) loop.iterate();
+    CHECK(ga.size() == sa.size() && gb.size() == sb.size());
+    for (size_t i = 0; i < ga.size() && i < sa.size(); ++i) CHECK(ga[i].payload == sa[i] && ga[i].opcode == 2);
+    for (size_t i = 0; i < gb.size() && i < sb.size(); ++i) CHECK(gb[i].payload == sb[i] && gb[i].opcode == 1);
+
+    // CLOSE on a: everything queued (b's frame too) is delivered before handleData returns CLOSED
+    {
+        const uint8_t key[4] = {9, 8, 7, 6};
+        std::vector<uint8_t> fb = masked_frame(2, std::string(777, 'q'), key);
+        CHECK(b.handleData(fb.data(), fb.size()) == WSError::NOERR);
+        std::vector<uint8_t> fa = masked_frame(1, "bye?", key);
+        std::vector<uint8_t> cl = masked_frame(8, std::string("\x03\xe8", 2), key);
+        fa.insert(fa.end(), cl.begin(), cl.end());
+        const size_t na = ga.size(), nb = gb.size();
+        CHECK(a.handleData(fa.data(), fa.size()) == WSError::CLOSED);
+        CHECK(ga.size() == na + 2 && ga[na].payload == "bye?" && ga[na + 1].opcode == 8);
+        CHECK(gb.size() == nb + 1 && gb[nb].payload == std::string(777, 'q'));
+    }
+    // a decode error: the frames before it are delivered first, then the error returns
+    {
+        const uint8_t key[4] = {1, 1, 2, 3};
+        std::vector<uint8_t> w = masked_frame(2, "first", key);
+        w.push_back(0x09);  // PING without FIN: PROTOCOL_ERROR (WSHandler.cpp:120-130)
+        w.push_back(0x80);
+        const size_t nb = gb.size();
+        CHECK(b.handleData(w.data(), w.size()) == WSError::PROTOCOL_ERROR);
+        CHECK(gb.size() == nb + 1 && gb[nb].payload == "first");
+    }
+    // a handler deleted by its own callback during deferred delivery
+    {
+        WSHandler* h = new WSHandler();
+        h->setMode(WSMode::SERVER);
+        h->setRxLoop(&rx);
+        int calls = 0;
+        h->setFrameCallback([&](FrameHeader, BufferChain&) {
+            ++calls;
+            delete h;
+            h = nullptr;
+            return 0;
+        });
+        const uint8_t key[4] = {4, 3, 2, 1};
+        std::vector<uint8_t> w = masked_frame(2, "one", key), w2 = masked_frame(2, "two", key);
+        w.insert(w.end(), w2.begin(), w2.end());
+        CHECK(h->handleData(w.data(), w.size()) == WSError::NOERR);
+        for (int spin = 0; spin < 100000 && (rx.inflight() || rx.pending() || !loop.tasks.empty()); ++spin)
+            loop.iterate();
+        CHECK(calls == 1 && h == nullptr);
+    }
+    // a handler destroyed while its frames are queued: they are dropped, nothing touches it
+    {
+        WSHandler* h = new WSHandler();
+        h->setMode(WSMode::SERVER);
+        h->setRxLoop(&rx);
+        int calls = 0;
+        h->setFrameCallback([&](FrameHeader, BufferChain&) {
+            ++calls;
+            return 0;
+        });
+        const uint8_t key[4] = {4, 3, 2, 1};
+        std::vector<uint8_t> w = masked_frame(2, "dropped", key);
+        CHECK(h->handleData(w.data(), w.size()) == WSError::NOERR);
+        delete h;
+        for (int spin = 0; spin < 100000 && (rx.inflight() || rx.pending() || !loop.tasks.empty()); ++spin)
+            loop.iterate();
+        CHECK(calls == 0);
+    }
+}
+
 static void nogpu_checks()
 {
+    {  // batched mode needs a device: the loop object is invalid and handlers stay synchronous
+        FakeLoop loop;
+        kmws::RxLoop rx(loop.poster(), 0);
+        CHECK(!rx.valid());
+        WSHandler h;
+        h.setRxLoop(&rx);
+        CHECK(h.rxLoop() == nullptr);
+    }
     WSHandler h;
     h.setMode(WSMode::SERVER);
     std::vector<Rec> got;
@@ -231,7 +376,11 @@ int main(int argc, char** argv)
 {
     host_checks();
     const std::string mode = argc > 1 ? argv[1] : "";
-    if (mode == "gpu") gpu_checks();
+    if (mode == "gpu") {
+        gpu_checks();
+        batched_checks(true);
+        batched_checks(false);
+    }
     if (mode == "nogpu") nogpu_checks();
     if (g_fail) {
         std::printf("%d checks failed\n", g_fail);

@@ -78,3 +78,57 @@ def test_cfg5_sub_batches_per_gpu_count():
     for world, nb in ((1, 8), (2, 4), (4, 2), (8, 1)):
         n, bs = shard.sub_batches(10485760, 0, world, 1310720)
         assert len(bs) == nb and n == 1310720
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def test_gpus_world_size_mismatch_is_refused():
+    """Under a launcher, --gpus N must equal WORLD_SIZE (one rank per GPU)."""
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_gpus_n_starts_n_ranks_itself():
+    """bench.py --gpus 2 without WORLD_SIZE starts 2 rank processes (torchrun's
+    environment, 127.0.0.1 rendezvous).  Without a GPU every rank refuses to run
+    (no CPU fallback) and the launcher returns a non-zero status; the GPU form
+    of this check is tests/test_gpu_bench_sharded.py."""
+    if _has_gpu():
+        return
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode != 0
+    assert r.stderr.count("no GPU visible") == 2, r.stderr
+
+
+def test_launch_ranks_environment(tmp_path):
+    """launch_ranks gives rank r RANK=LOCAL_RANK=r, WORLD_SIZE=N and one shared
+    127.0.0.1 rendezvous port, re-running the same script with the same argv."""
+    script = tmp_path / "probe.py"
+    script.write_text(
+        "import os, sys, json\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import bench\n"
+        "if 'WORLD_SIZE' not in os.environ:\n"
+        "    bench.__file__ = __file__\n"
+        "    sys.exit(bench.launch_ranks(3))\n"
+        "print(json.dumps({k: os.environ[k] for k in ('RANK','LOCAL_RANK','WORLD_SIZE','MASTER_ADDR','MASTER_PORT')}"
+        " | {'argv': sys.argv[1:]}))\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(script), "--x", "1"], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    rows = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert sorted(int(x["RANK"]) for x in rows) == [0, 1, 2]
+    assert all(x["RANK"] == x["LOCAL_RANK"] and x["WORLD_SIZE"] == "3" and x["MASTER_ADDR"] == "127.0.0.1"
+               for x in rows)
+    assert len({x["MASTER_PORT"] for x in rows}) == 1 and all(x["argv"] == ["--x", "1"] for x in rows)

@@ -1,5 +1,6 @@
 """C-ABI checks that need no GPU: the library loads and exports every symbol
-include/kmws_gpu.h declares; host codec entries match the oracle."""
+include/kmws_gpu.h and include/kmws_bench.h declare; host codec entries match
+the oracle."""
 import os
 import random
 import re
@@ -12,8 +13,8 @@ from oracle import oracle as orc
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_decls():
-    txt = open(os.path.join(ROOT, "include", "kmws_gpu.h")).read()
+def header_decls(name="kmws_gpu.h"):
+    txt = open(os.path.join(ROOT, "include", name)).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     names = set(re.findall(r"\b(kmws_[a-z0-9_]+)\s*\(", txt))
     return sorted(n for n in names if n != "kmws_make_flags")  # static inline helper
@@ -26,6 +27,21 @@ def test_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(L, name), name
     assert sorted(kmws.EXPORTS) == decl
+    bench = header_decls("kmws_bench.h")
+    for name in bench:
+        assert hasattr(L, name), name
+    assert sorted(kmws.BENCH_EXPORTS) == bench
+
+
+def test_public_header_has_no_tuning_entries():
+    """The drop-in header carries only boundary entries: no tuning variants,
+    no device-global schedule query, no persistent-grid probes."""
+    decl = header_decls()
+    for gone in ("kmws_unmask_batch_variant", "kmws_unmask_schedule", "kmws_unmask_resident_blocks",
+                 "kmws_arena_alloc", "kmws_fill_synthetic"):
+        assert gone not in decl
+    L = kmws.lib()
+    assert not hasattr(L, "kmws_unmask_batch_variant") and not hasattr(L, "kmws_unmask_resident_blocks")
 
 
 def test_encode_header_matches_oracle():

@@ -1,0 +1,55 @@
+"""GPU: the sharded HIP path of bench.py (BASELINE configs[4], SURVEY 8 e).
+
+`bench.py --gpus 2 --dist-backend gloo` starts its two rank processes itself
+(one GPU per rank; on a one-GPU box both share it), each rank generates its
+own shard of a fixed job on the device, unmasks it with the product kernels
+in resident sub-batches, and verifies every byte with the device checker.
+The test reads rank 0's JSON line: two ranks, contiguous shards covering the
+job, sub-batches covering each shard, no mismatches, a clean status word."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("job,max_batch", [(65536, 16384), (50001, 20000)])
+def test_bench_two_ranks_shard_the_job(job, max_batch):
+    d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--job-frames", str(job), "--max-batch-frames",
+                  str(max_batch), "--steps", "3", "--warmup", "1", "--cpu-seconds", "0")
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["verify"]["byte_mismatches"] == 0 and d["verify"]["status_word"] == 0
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert ranks[0]["frames"][0] == 0 and ranks[-1]["frames"][1] == job
+    assert ranks[0]["frames"][1] == ranks[1]["frames"][0]
+    for r in ranks:
+        subs = r["sub_batches"]
+        assert subs[0][0] == r["frames"][0] and subs[-1][1] == r["frames"][1]
+        assert all(a[1] == b[0] for a, b in zip(subs, subs[1:]))
+        assert all(hi - lo <= max_batch for lo, hi in subs)
+        assert r["byte_mismatches"] == 0
+    assert len({len(r["sub_batches"]) for r in ranks}) == 1  # the barriers pair up
+    assert d["value"] > 0 and d["config"]["total_frames"] == job
+
+
+def test_bench_one_gpu_small_batch_plain_rate():
+    """N = 1 weak scaling on a small batch: the JSON line carries the plain
+    allocation's rate only when an arena was placed (too small here: none)."""
+    d = run_bench("--frames", "16384", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0")
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["verify"]["byte_mismatches"] == 0
+    assert d["config"]["placement"]["kind"] == "plain torch.empty"
+    assert d["roofline"]["frac_plain"] is None and d["roofline"]["frac"] > 0

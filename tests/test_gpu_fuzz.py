@@ -25,8 +25,8 @@ from oracle import oracle as orc
 
 pytestmark = pytest.mark.gpu
 BUDGET = float(os.environ.get("KMWS_FUZZ_SECONDS", "8"))
-SCHEDULES = [None, 0, 23, 21, 27, 36, 3, 10,  # product default, in order, splits, XCD runs, persistent grids
-             5 | 1 << 30, 3 | 1 << 30]         # split 4 / split 8 with temporal stores
+# product default + every placement kind with automatic, non-temporal and temporal stores
+SCHEDULES = [None] + [k | s for k in range(6) for s in (0, 1 << 29, 1 << 30)]
 
 
 @pytest.fixture(scope="module")
@@ -86,11 +86,11 @@ def test_fuzz_unmask(T):
         d_desc = T.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).cuda()
         ws = kmws.Workspace(kmws.unmask_workspace_size(total))
         v = SCHEDULES[int(rng.integers(0, len(SCHEDULES)))]
-        kmws.unmask_batch(d_buf, d_desc, ws, total, variant=v)
+        kmws.unmask_batch(d_buf, d_desc, ws, total, schedule=v)
         T.cuda.synchronize()
-        assert ws.status() == 0, f"status (variant {v})"
+        assert ws.status() == 0, f"status (schedule {v})"
         got = d_buf.cpu().numpy()[:total]
-        assert np.array_equal(got, want), f"bytes differ (variant {v}, n {n})"
+        assert np.array_equal(got, want), f"bytes differ (schedule {v}, n {n})"
 
     print("unmask cases:", budget_loop(case))
 

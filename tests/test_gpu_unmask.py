@@ -23,7 +23,7 @@ def torch_dev():
     return torch
 
 
-def run_gpu(torch, buf: np.ndarray, descs: np.ndarray, span=None, variant=None, stream=None):
+def run_gpu(torch, buf: np.ndarray, descs: np.ndarray, span=None, schedule=None, stream=None):
     from kuma_amd import kmws
     span = len(buf) if span is None else span
     pad = (-len(buf)) % 16
@@ -31,9 +31,12 @@ def run_gpu(torch, buf: np.ndarray, descs: np.ndarray, span=None, variant=None, 
     d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda() if len(descs) else \
         torch.zeros((0, 2), dtype=torch.int64, device="cuda")
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
-    kmws.unmask_batch(d_buf, d_desc, ws, span, variant=variant, stream=stream)
+    kmws.unmask_batch(d_buf, d_desc, ws, span, schedule=schedule, stream=stream)
     torch.cuda.synchronize()
     return d_buf.cpu().numpy()[:len(buf)], ws.status()
+
+
+KINDS_X_STORES = [k | s for k in range(6) for s in (0, 1 << 29, 1 << 30)]  # placement kind x auto / NT / temporal
 
 
 def make_descs(offs, lens, keys):
@@ -108,14 +111,13 @@ KINDS = ["aligned64k", "packed_wire", "zipf_mixed", "tiny_many", "zero_len_runs"
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 66, 65537, 2097152,
-                                     1 << 30, 2 | 1 << 30, 3 | 1 << 30, 4 | 1 << 30, 5 | 1 << 30])  # temporal stores
-def test_unmask_parity(torch_dev, kind, variant):
-    rng = np.random.default_rng(zlib.crc32(f"{kind}-{variant}".encode()))
+@pytest.mark.parametrize("schedule", [None] + KINDS_X_STORES)
+def test_unmask_parity(torch_dev, kind, schedule):
+    rng = np.random.default_rng(zlib.crc32(f"{kind}-{schedule}".encode()))
     buf, descs = layout(kind, rng)
     want = buf.copy()
     orc.unmask_batch(want, descs)
-    got, st = run_gpu(torch_dev, buf, descs, variant=variant)
+    got, st = run_gpu(torch_dev, buf, descs, schedule=schedule)
     assert st == 0
     assert np.array_equal(got, want)
 
@@ -202,30 +204,91 @@ def test_unmask_on_side_stream(torch_dev):
     assert st == 0 and np.array_equal(got, want)
 
 
+def _to_dev(torch, buf, descs):
+    d_buf = torch.from_numpy(np.concatenate([buf, np.zeros((-len(buf)) % 16, np.uint8)])).cuda()
+    d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
+    return d_buf, d_desc
+
+
+def _valid_schedule(code):
+    store = code & (3 << 29)
+    return (code & 0xFF) in range(6) and store != 3 << 29 and code & ~(0xFF | 3 << 29) == 0
+
+
 def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     """kmws_unmask_autotune runs every schedule twice (XOR twice = identity):
-    the payload is unchanged, and unmask parity holds under the chosen schedule."""
+    the payload is unchanged, the pick is recorded for THIS batch only, and
+    unmask parity holds under it."""
     torch = torch_dev
     from kuma_amd import kmws
     rng = np.random.default_rng(31)
     buf, descs = layout("packed_wire", rng)
-    d_buf = torch.from_numpy(np.concatenate([buf, np.zeros((-len(buf)) % 16, np.uint8)])).cuda()
-    d_desc = torch.from_numpy(descs.view(np.int64).reshape(-1, 2).copy()).cuda()
+    d_buf, d_desc = _to_dev(torch, buf, descs)
     ws = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     choice = kmws.unmask_autotune(d_buf, d_desc, ws, len(buf))
-    assert (choice in (0, 1, 2, 3, 4, 5) or (choice & ~(1 << 30)) in (0, 2, 3, 4, 5)) and kmws.unmask_schedule() == choice
+    assert _valid_schedule(choice) and choice & (3 << 29)  # the autotune times forced store policies
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == choice
+    ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS  # other batches: default
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.SCHED_GROUPED_RUNS  # other span
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
-    got, st = run_gpu(torch, buf, descs)
-    assert st == 0 and np.array_equal(got, want)
+    kmws.unmask_batch(d_buf, d_desc, ws, len(buf))
+    torch.cuda.synchronize()
+    assert ws.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
+    kmws.unmask_set_schedule(ws, d_desc, len(buf), -1)  # forget: back to the default
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS
+
+
+def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
+    """ADVICE r02 / VERDICT r02 #4: tuning an aligned arena (which may pick
+    temporal stores) must not change how a packed wire image is unmasked later
+    in the same process: the wire keeps the default schedule, and the plan's
+    layout flag (workspace word 1) makes its automatic store policy
+    non-temporal; the aligned batch's flag selects temporal stores."""
+    torch = torch_dev
+    from kuma_amd import kmws
+    n, L = 4096, 65536
+    span = n * L
+    base = torch.empty(span, dtype=torch.uint8, device="cuda")
+    descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    kmws.fill_synthetic(base, 5)
+    kmws.fill_uniform_descs(descs, L, L, 6)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(span))
+    kmws.unmask_autotune(base, descs, ws, span)
+    kmws.unmask_plan(descs, ws, span)
+    torch.cuda.synchronize()
+    assert int(ws.tensor[4:8].cpu().view(torch.int32)[0]) == 0  # every frame on a tile boundary
+    rng = np.random.default_rng(77)
+    buf, wd = layout("packed_wire", rng)
+    d_buf, d_desc = _to_dev(torch, buf, wd)
+    ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS
+    want = buf.copy()
+    orc.unmask_batch(want, wd)
+    kmws.unmask_batch(d_buf, d_desc, ws2, len(buf))
+    torch.cuda.synchronize()
+    assert int(ws2.tensor[4:8].cpu().view(torch.int32)[0]) == 1  # unaligned: automatic stores are non-temporal
+    assert ws2.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
+    kmws.unmask_batch(base, descs, ws, span)  # the aligned batch under its tuned schedule
+    assert ws.status() == 0 and kmws.check_unmasked(base, 5, descs) == 0
+
+
+def test_set_schedule_rejects_bad_codes(torch_dev):
+    from kuma_amd import kmws
+    ws = kmws.Workspace(1024)
+    d = torch_dev.zeros((1, 2), dtype=torch.int64, device="cuda")
+    for bad in (6, 64, 0xFF, (1 << 29) | (1 << 30), 1 << 28, 65537):
+        assert kmws.lib().kmws_unmask_set_schedule(ws.ptr, d.data_ptr(), 1, 64, bad) == kmws.ERR_INVALID_PARAM
+    assert kmws.lib().kmws_unmask_set_schedule(None, d.data_ptr(), 1, 64, 0) == kmws.ERR_INVALID_PARAM
 
 
 @pytest.mark.parametrize("frame_len,tail", [(65536, 0), (65531, 0), (3000, 0), (65531, 7 * 16384 + 100)])
-@pytest.mark.parametrize("variant", [None, 4, 10, 21, 22, 23, 24, 25, 27, 29, 30, 36, 37, 38, 40, 41, 2097152, 65537])
-def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len, tail):
-    """512 MiB arena (32 K tiles: many tiles per block of the persistent
-    schedules, whole runs and parts of the XCD-run and split mappings), plus a
+@pytest.mark.parametrize("schedule", [None] + KINDS_X_STORES)
+def test_unmask_schedules_many_tiles_per_block(torch_dev, schedule, frame_len, tail):
+    """512 MiB arena (32 K tiles: whole runs and parts of the XCD-run and split
+    mappings), plus a
     tail that is not a whole number of runs / parts (and a partial last tile):
     payload generated on the device, every byte checked on the device against
     the generator (payload ^ key inside frames, untouched gaps).  Applied three
@@ -241,16 +304,10 @@ def test_unmask_schedules_many_tiles_per_block(torch_dev, variant, frame_len, ta
     kmws.fill_uniform_descs(descs, stride, frame_len, 99)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
     for _ in range(3):
-        kmws.unmask_batch(base, descs, ws, span, variant=variant)
+        kmws.unmask_batch(base, descs, ws, span, schedule=schedule)
     torch.cuda.synchronize()
     assert ws.status() == 0
     assert kmws.check_unmasked(base, 1234, descs) == 0
-
-
-def test_resident_blocks_reported(torch_dev):
-    from kuma_amd import kmws
-    r = kmws.unmask_resident_blocks()
-    assert r > 0 and r % torch_dev.cuda.get_device_properties(0).multi_processor_count == 0
 
 
 def test_arena_alloc_unmask_roundtrip(torch_dev):

@@ -475,7 +475,8 @@ def cfg4(reps: int, messages: int, placed: bool = True):
     torch.cuda.synchronize()
     w = wire[:P + H].view(n, L + 8)[:, 8:]
     verified = bool(torch.equal(w.reshape(-1), src[:P]))
-    t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), reps)
+    # even: the wire ends unmasked, the state the placed copy below starts from
+    t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), 2 * (reps // 2) + 2)
     placed_rec = None
     if placed:  # the same in-place unmask on a copy of the wire in a placement-probed arena (as bench.py)
         arena, pw, rec = placed_buffer(torch, kmws, P + H)
