@@ -278,7 +278,7 @@ def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
 def test_set_schedule_rejects_bad_codes(torch_dev):
     from kuma_amd import kmws
     ws = kmws.Workspace(1024)
-    d = torch_dev.zeros((1, 2), dtype=torch.int64, device="cuda")
+    d = torch_dev.zeros((1, 2), dtype=torch_dev.int64, device="cuda")
     for bad in (6, 64, 0xFF, (1 << 29) | (1 << 30), 1 << 28, 65537):
         assert kmws.lib().kmws_unmask_set_schedule(ws.ptr, d.data_ptr(), 1, 64, bad) == kmws.ERR_INVALID_PARAM
     assert kmws.lib().kmws_unmask_set_schedule(None, d.data_ptr(), 1, 64, 0) == kmws.ERR_INVALID_PARAM

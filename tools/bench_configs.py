@@ -475,8 +475,9 @@ def cfg4(reps: int, messages: int, placed: bool = True):
     torch.cuda.synchronize()
     w = wire[:P + H].view(n, L + 8)[:, 8:]
     verified = bool(torch.equal(w.reshape(-1), src[:P]))
-    # even: the wire ends unmasked, the state the placed copy below starts from
-    t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), 2 * (reps // 2) + 2)
+    # odd whatever --reps: the wire ends masked again, the state the placed copy
+    # below starts from (its odd pass count then leaves it unmasked)
+    t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), 2 * (reps // 2) + 1)
     placed_rec = None
     if placed:  # the same in-place unmask on a copy of the wire in a placement-probed arena (as bench.py)
         arena, pw, rec = placed_buffer(torch, kmws, P + H)
@@ -521,6 +522,8 @@ def cfg4(reps: int, messages: int, placed: bool = True):
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12, "placed": placed_rec},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
             "device_header_walk_by_streams": walk,
+            "verified_parts": {"unmask_in_place": verified, "encode_iovec": ok_iov,
+                               "placed": placed_rec["verified"] if placed_rec else None},
             "verified": verified and ok_iov}
 
 
