@@ -96,6 +96,9 @@ public:
 
     bool valid() const { return batch_ != nullptr; }
     kmws_rx_batch* batch() const { return batch_; }
+    // (Re)binds the loop's post function (e.g. when the loop object is created
+    // before its event loop runs).
+    void setPoster(Poster post) { post_ = std::move(post); }
 
     // Pinned receive ring the loop reads sockets into (kmws_host_alloc): payloads
     // lying in it are unmasked there, without copies.  Ring bytes of a frame

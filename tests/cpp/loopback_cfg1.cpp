@@ -11,10 +11,18 @@
 //        kmws_rx_batch_flush per loop iteration (socket drained to EAGAIN).
 //        The batches and rings belong to the loop threads (created once); the
 //        decoder is per connection, as kuma's WSHandler.
+//   adapter  the drop-in as kuma would run it: the server
+//        holds a kmws::BasicWSHandler (include/kmws_wshandler.hpp) in batched
+//        mode -- handleData per read, as WebSocket::Impl::onWsData calls it,
+//        frames queued on the loop thread's kmws::RxLoop, whose posted task
+//        submits the iteration's unmask and delivers finished generations at the
+//        next iterations (asynchronous, the GPU round trip overlaps the reads);
+//        the client submits each iteration's masks (kmws_tx_batch_submit) and
+//        writes the previous iteration's frames while they run (two send slots).
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu [reps]
+// usage: loopback_cfg1 cpu|gpu|adapter [reps] [frames per send iteration] [rx flush bytes]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -35,6 +43,7 @@
 #include <vector>
 
 #include "kmws_gpu.h"
+#include "kmws_wshandler.hpp"
 
 extern "C" {  // oracle/kmws_oracle.c (test infrastructure)
 typedef struct orc_hdr {
@@ -132,10 +141,11 @@ struct LoopObjs {
     uint8_t* rring = nullptr;
     kmws_tx_batch* tx = nullptr;
     uint8_t* sring = nullptr;
+    kmws::RxLoop* rxloop = nullptr;  // adapter mode: the server loop's RxLoop (owns its own batch)
 };
 
 // One connection: returns seconds from the first send to the last delivered frame.
-double run_once(bool gpu, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
+double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
     int ls = socket(AF_INET, SOCK_STREAM, 0);
     sockaddr_in a{};
@@ -158,7 +168,7 @@ double run_once(bool gpu, Expect& e, const std::vector<uint32_t>& keys, const Lo
         int one = 1;
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
         ready = true;
-        if (gpu) {
+        if (gpu && !adapter) {
             kmws_decoder* d = kmws_decoder_create(KMWS_MODE_SERVER, 0);  // per connection, as in kuma
             kmws_rx_batch* b = lo.rx;
             uint8_t* ring = lo.rring;
@@ -192,6 +202,53 @@ double run_once(bool gpu, Expect& e, const std::vector<uint32_t>& keys, const Lo
                 pos = 0;  // ring bytes are free again after the flush
             }
             kmws_decoder_destroy(d);
+        } else if (adapter) {
+            // the loop thread: its RxLoop (posted tasks run once per iteration) and ring
+            std::vector<kmws::RxLoop::Task> tasks;
+            kmws::RxLoop& rx = *lo.rxloop;
+            rx.setPoster([&tasks](kmws::RxLoop::Task t) { tasks.push_back(std::move(t)); });
+            kmws::ws::WSHandler h;  // per connection: WebSocket::Impl's ws_handler_
+            h.setMode(kmws::ws::WSMode::SERVER);
+            h.setRxLoop(&rx);
+            h.setFrameCallback([&e](kmws::ws::FrameHeader hdr, kmws::ws::BufferChain& buf) {
+                check_frame(&e, static_cast<const uint8_t*>(buf.readPtr()), buf.length(), hdr.opcode);
+                return 0;
+            });
+            uint8_t* ring = lo.rring;
+            size_t pos = 0;
+            bool closed = false;
+            while (e.got.load(std::memory_order_acquire) < kFrames) {
+                // one loop iteration: reads until the socket is drained (blocking only
+                // when nothing is queued or in flight), then the posted tasks
+                const bool busy = !tasks.empty() || rx.inflight() > 0 || rx.pending() > 0;
+                int flags = busy || closed ? MSG_DONTWAIT : 0;
+                for (;;) {
+                    if (pos + kRead > kRing) {  // wrap: ring bytes are free once every frame was delivered
+                        const double tf = now_s();
+                        if (rx.flush() < 0) std::exit(5);
+                        g_t.rx_flush += now_s() - tf;
+                        pos = 0;
+                    }
+                    double t = now_s();
+                    const ssize_t r = closed ? -1 : recv(fd, ring + pos, kRead, flags);
+                    g_t.recv += now_s() - t;
+                    if (r == 0) closed = true;
+                    if (r <= 0) break;
+                    t = now_s();
+                    const kmws::ws::WSError err = h.handleData(ring + pos, (size_t)r);  // onWsData
+                    g_t.rx_feed += now_s() - t;
+                    if (err != kmws::ws::WSError::NOERR && err != kmws::ws::WSError::NEED_MORE_DATA) std::exit(4);
+                    pos += (size_t)r;
+                    flags = MSG_DONTWAIT;
+                }
+                const double tf = now_s();
+                std::vector<kmws::RxLoop::Task> now;
+                now.swap(tasks);
+                for (auto& t : now) t();
+                if (rx.lastResult() < 0) std::exit(5);
+                g_t.rx_flush += now_s() - tf;
+                if (closed && tasks.empty() && rx.inflight() == 0 && rx.pending() == 0) break;
+            }
         } else {
             orc_decoder* d = orc_decoder_create(1);
             std::vector<uint8_t> buf(kRead);
@@ -223,7 +280,54 @@ double run_once(bool gpu, Expect& e, const std::vector<uint32_t>& keys, const Lo
     std::vector<int> hlen(kGroup);
     std::vector<iovec> iov;
     const auto t0 = std::chrono::steady_clock::now();
-    for (int g0 = 0; g0 < kFrames; g0 += kGroup) {
+    if (adapter) {
+        // two send slots: iteration k fills and submits slot k % 2, then writes
+        // iteration k - 1 once its masks completed
+        std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hd[2] = {hdrs, hdrs};
+        std::vector<int> hl[2] = {hlen, hlen};
+        int64_t ticket[2] = {0, 0};
+        int count[2] = {0, 0};
+        auto write_slot = [&](int sl) {
+            double tt = now_s();
+            if (kmws_tx_batch_poll(tx, ticket[sl], 1) != 1) std::exit(7);
+            g_t.tx_flush += now_s() - tt;
+            iov.clear();
+            uint8_t* base = sring + (size_t)sl * kGroup * kLen;
+            for (int j = 0; j < count[sl]; ++j) {
+                iov.push_back(iovec{hd[sl][j].data(), (size_t)hl[sl][j]});
+                iov.push_back(iovec{base + (size_t)j * kLen, kLen});
+            }
+            tt = now_s();
+            send_all(fd, iov);
+            g_t.writev += now_s() - tt;
+        };
+        int k = 0;
+        for (int g0 = 0; g0 < kFrames; g0 += kGroup, ++k) {
+            const int sl = k & 1, ng = std::min(kGroup, kFrames - g0);
+            uint8_t* base = sring + (size_t)sl * kGroup * kLen;
+            std::memcpy(base, e.plain.data() + (size_t)g0 * kLen, (size_t)ng * kLen);
+            for (int j = 0; j < ng; ++j) {
+                uint8_t* p = base + (size_t)j * kLen;
+                const uint32_t key = keys[g0 + j];
+                kmws_frame_hdr h;
+                std::memset(&h, 0, sizeof h);
+                h.fin = 1;
+                h.opcode = KMWS_OP_TEXT;
+                h.mask = 1;
+                std::memcpy(h.maskey, &key, 4);
+                size_t len = kLen;
+                hl[sl][j] = kmws_tx_batch_add(tx, &h, &p, &len, 1, hd[sl][j].data());
+            }
+            double tt = now_s();
+            ticket[sl] = kmws_tx_batch_submit(tx);
+            g_t.tx_flush += now_s() - tt;
+            if (ticket[sl] <= 0) std::exit(7);
+            count[sl] = ng;
+            if (k > 0) write_slot(sl ^ 1);
+        }
+        if (k > 0) write_slot((k - 1) & 1);
+    }
+    for (int g0 = 0; g0 < kFrames && !adapter; g0 += kGroup) {
         const int ng = std::min(kGroup, kFrames - g0);
         uint8_t* base = gpu ? sring : sbuf.data();
         // the application writes its payloads (the send buffer is reused per iteration)
@@ -279,7 +383,8 @@ int main(int argc, char** argv)
     const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
     if (argc > 3) kGroup = std::max(1, std::atoi(argv[3]));
     if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
-    const bool gpu = mode == "gpu";
+    const bool adapter = mode == "adapter";
+    const bool gpu = mode == "gpu" || adapter;
     if (gpu && kmws_device_count() < 1) {
         std::printf("{\"mode\": \"gpu\", \"error\": \"no gfx950 device\"}\n");
         return 1;
@@ -294,19 +399,25 @@ int main(int argc, char** argv)
         lo.rx = kmws_rx_batch_create(0);
         lo.rring = static_cast<uint8_t*>(kmws_host_alloc(kRing, 0));
         lo.tx = kmws_tx_batch_create(0);
-        lo.sring = static_cast<uint8_t*>(kmws_host_alloc((size_t)kGroup * kLen, 0));
-        if (!lo.rx || !lo.rring || !lo.tx || !lo.sring || kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK ||
-            kmws_tx_batch_attach_ring(lo.tx, lo.sring, (size_t)kGroup * kLen) != KMWS_OK)
+        lo.sring = static_cast<uint8_t*>(kmws_host_alloc((size_t)2 * kGroup * kLen, 0));  // 2 slots (adapter)
+        if (!lo.rx || !lo.rring || !lo.tx || !lo.sring || kmws_tx_batch_attach_ring(lo.tx, lo.sring, (size_t)2 * kGroup * kLen) != KMWS_OK)
             return 3;
+        if (adapter) {
+            lo.rxloop = new kmws::RxLoop(nullptr, 0);
+            if (!lo.rxloop->valid() || lo.rxloop->attachRing(lo.rring, kRing) != KMWS_OK) return 3;
+        } else if (kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK) {
+            return 3;
+        }
     }
     double best = 1e9;
     bool ok = true;
     for (int r = 0; r < reps + 1; ++r) {  // first connection warms up (staging growth, GPU context)
-        const double t = run_once(gpu, e, keys, lo);
+        const double t = run_once(gpu, adapter, e, keys, lo);
         ok = ok && e.got.load() == kFrames && e.bad.load() == 0;
         if (r) best = std::min(best, t);
     }
     if (gpu) {
+        delete lo.rxloop;
         kmws_rx_batch_destroy(lo.rx);
         kmws_tx_batch_destroy(lo.tx);
         kmws_host_free(lo.rring);

@@ -111,3 +111,18 @@ def test_loopback_cfg1_gpu_codec(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["verified"] and d["frames"] == 1000
+
+
+@pytest.mark.gpu
+def test_loopback_cfg1_adapter_batched(tmp_path):
+    """The drop-in in batched mode over loopback: kmws::BasicWSHandler with an
+    RxLoop (asynchronous submit / poll once per loop iteration) on the server,
+    submitted tx generations on the client; every payload delivered intact, in
+    order, at 64 KiB and 256 KiB per loop iteration."""
+    import json
+    exe = _build_loopback(tmp_path)
+    for group in ("16", "64"):
+        r = subprocess.run([str(exe), "adapter", "2", group], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["verified"] and d["frames"] == 1000 and d["mode"] == "adapter"
