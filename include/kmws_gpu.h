@@ -244,12 +244,12 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
 /* Unmask schedules.  The apply grid is one block per 16 KiB tile; a schedule
  * says which tiles the resident blocks stream at once and how the payload is
  * stored.  Placement kind (low byte): */
-#define KMWS_SCHED_GROUPED_RUNS 0   /* XCDs in 2 groups, runs of 16 tiles in each group's half (default) */
+#define KMWS_SCHED_GROUPED_RUNS 0   /* XCDs in 2 groups, runs of 16 tiles in each group's half */
 #define KMWS_SCHED_IN_ORDER     1   /* tile = block */
 #define KMWS_SCHED_SPLIT2       2   /* blocks dealt over 2 far-apart parts of the span */
 #define KMWS_SCHED_SPLIT8       3   /* ... over 8 parts */
 #define KMWS_SCHED_XCD_RUNS     4   /* runs of 16 tiles per XCD */
-#define KMWS_SCHED_SPLIT4       5   /* ... over 4 parts */
+#define KMWS_SCHED_SPLIT4       5   /* ... over 4 parts (the default) */
 /* Store policy (at most one bit; neither = automatic: temporal stores when every
  * frame of the batch starts on a 16 KiB tile boundary -- the plan records the
  * layout -- non-temporal otherwise, e.g. for a packed wire image). */
@@ -261,7 +261,7 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * applied twice leaves the payload unchanged), times them with events on
  * `stream` (synchronizes) and records the fastest for this batch -- the tuple
  * (workspace, descs, n, span) -- where kmws_unmask_apply / kmws_unmask_batch
- * find it.  Every other batch keeps the default schedule (grouped runs,
+ * find it.  Every other batch keeps the default schedule (split 4,
  * automatic stores): no device-global state.  Returns the chosen schedule code
  * or a negative status. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,

@@ -18,7 +18,8 @@ constexpr int kBlock = 256;          // 4 waves of 64 lanes
 struct WsHead {
     uint32_t status;
     uint32_t layout;  // kLayout* bits, written by the unmask plan
-    uint32_t pad[2];
+    uint32_t ticket;  // tile tickets of the single-pass scan (kmws_pack.hip)
+    uint32_t pad;
 };
 constexpr uint32_t kStatusBadDesc = 1u;
 constexpr uint32_t kStatusBadHeader = 2u;

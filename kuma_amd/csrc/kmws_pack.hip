@@ -4,7 +4,7 @@
 // (src/ws/WSHandler.cpp:46-106) followed by the masked payload
 // (WebSocket::Impl::sendWsFrame, src/ws/WebSocketImpl.cpp:381-404): the wire
 // image is header_0 payload_0 header_1 payload_1 ...  Kernels:
-//   1. scan_reduce / scan_partials / scan_emit: one exclusive scan of two
+//   1. scan_kernel: one single-pass (decoupled look-back) exclusive scan of two
 //      per-frame values -- the wire size (2/4/10 + 4*mask + len) -> wire_off,
 //      and an upper bound on the frame's wave units -> unit slot bases;
 //   2. prologue_kernel, 256 frames per block: the few words around each
@@ -149,72 +149,92 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x)
     return x;
 }
 
-// Frames of a scan block are read row-striped (frame base + i*kBlock + tid), so
-// every load instruction is coalesced.
-template <class Size>
-__global__ void __launch_bounds__(kBlock) scan_reduce_kernel(Size size, uint32_t n, V2* __restrict__ partials)
+// Single-pass scan (decoupled look-back).  A block scans 2048 frames, read
+// row-striped (frame base + i*kBlock + tid) so every load is coalesced.  Blocks
+// take their tile in ticket order (an atomic counter in the workspace head),
+// publish their tile's aggregate at once and its inclusive prefix as soon as
+// their look-back resolved: a block only ever waits on blocks that started
+// before it, so the grid always makes progress, and one launch replaces the
+// reduce / scan-partials / emit launches (and the second read of the
+// descriptors) of a three-pass scan.  Tile state: per quantity one 64-bit word,
+// (flag << 62) | value, written and read with device-scope atomics (the L2s of
+// the 8 XCDs are not coherent for plain accesses); a state is taken when both
+// words carry the same flag.
+struct ScanState {
+    uint64_t a, b;
+};
+constexpr uint64_t kFlagAgg = 1ull, kFlagInc = 2ull, kValMask = (1ull << 62) - 1;
+constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.1-1 s: a lost predecessor sets the status instead of hanging
+
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
 {
-    __shared__ V2 s_wave[kBlock / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
-    V2 s{0, 0};
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        const uint64_t f = base + (uint64_t)i * kBlock;
-        if (f < n) s = s + size((uint32_t)f);
-    }
-    s.a = wave_sum(s.a);
-    s.b = wave_sum(s.b);
-    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        V2 t{0, 0};
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) t = t + s_wave[w];
-        partials[blockIdx.x] = t;
-    }
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish(ScanState* st, uint64_t flag, V2 v)
+{
+    st_agent(&st->a, flag << 62 | (v.a & kValMask));
+    st_agent(&st->b, flag << 62 | (v.b & kValMask));
 }
 
-// One block scans the per-block totals in place (exclusive) and writes the grand totals.
-__global__ void __launch_bounds__(kBlock) scan_partials_kernel(V2* __restrict__ partials, uint32_t nb,
-                                                               uint64_t* __restrict__ total_a,
-                                                               uint64_t* __restrict__ total_b)
+// Wave 0 of tile `tile`: the exclusive prefix of the tiles before it.  Lane l
+// looks at tile j - l of a 64-tile window; the window's tiles up to and
+// including the nearest one with an inclusive prefix contribute (nonexistent
+// tiles below 0 count as an inclusive zero); without one the window's
+// aggregates are summed and the window moves 64 tiles back.
+__device__ V2 look_back(const ScanState* __restrict__ st, uint32_t tile, WsHead* __restrict__ head)
 {
-    __shared__ V2 s_wave[kBlock / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    V2 carry{0, 0};
-    for (uint32_t base = 0; base < nb; base += kBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const V2 x = i < nb ? partials[i] : V2{0, 0};
-        const V2 inc{wave_incl_scan(x.a), wave_incl_scan(x.b)};
-        if (lane == 63) s_wave[wave] = inc;
-        __syncthreads();
-        V2 before{0, 0}, tot{0, 0};
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const V2 v = s_wave[w];
-            if (w < wave) before = before + v;
-            tot = tot + v;
+    const int lane = threadIdx.x & 63;
+    V2 ex{0, 0};
+    for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64) {
+        const int64_t p = j - lane;
+        uint64_t kind = kFlagInc, va = 0, vb = 0;
+        if (p >= 0) {
+            for (uint32_t spins = 0;; ++spins) {
+                const uint64_t A = ld_agent(&st[p].a), B = ld_agent(&st[p].b);
+                if ((A >> 62) != 0 && (A >> 62) == (B >> 62)) {
+                    kind = A >> 62;
+                    va = A & kValMask;
+                    vb = B & kValMask;
+                    break;
+                }
+                if (spins >= kSpinLimit) {  // cannot happen: every ticketed tile publishes
+                    atomicOr(&head->status, kStatusBadDesc);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
-        __syncthreads();
-        if (i < nb) partials[i] = V2{carry.a + before.a + inc.a - x.a, carry.b + before.b + inc.b - x.b};
-        carry = carry + tot;
+        const uint64_t inc = __ballot(kind == kFlagInc);
+        const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+        const bool take = lane <= first;
+        ex.a += wave_sum(take ? va : 0);
+        ex.b += wave_sum(take ? vb : 0);
+        if (inc) break;
     }
-    if (threadIdx.x == 0) {
-        *total_a = carry.a;
-        *total_b = carry.b;
-    }
+    return ex;
 }
 
-// (hdr != nullptr: also frame f's header bytes into the 16-byte slot hdr[f] and
-// its length into hl_out[f] -- kmws_pack_headers; Size is WireSize then)
+// Region offsets -> out_a (n+1 entries, out_a[n] = total), unit slot bases ->
+// out_b.  (hdr != nullptr: also frame f's header bytes into the 16-byte slot
+// hdr[f] and its length into hl_out[f] -- kmws_pack_headers; Size is WireSize.)
 template <class Size>
-__global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n, const V2* __restrict__ partials,
-                                                           uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b,
-                                                           u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
+__global__ void __launch_bounds__(kBlock) scan_kernel(Size size, uint32_t n, uint32_t ntiles,
+                                                      ScanState* __restrict__ st, WsHead* __restrict__ head,
+                                                      uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b,
+                                                      u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
 {
     __shared__ V2 s_row[kScanItems][kBlock / 64];
+    __shared__ V2 s_prefix;
+    __shared__ uint32_t s_tile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(&head->ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x;
+    const uint64_t base = (uint64_t)tile * kScanTile + threadIdx.x;
     V2 ex[kScanItems];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
@@ -225,8 +245,31 @@ __global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n
         if (lane == 63) s_row[i][wave] = inc;
     }
     __syncthreads();
+    if (wave == 0) {
+        V2 agg{0, 0};
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i)
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) agg = agg + s_row[i][w];
+        V2 pre{0, 0};
+        if (tile == 0) {
+            if (lane == 0) publish(&st[0], kFlagInc, agg);
+        } else {
+            if (lane == 0) publish(&st[tile], kFlagAgg, agg);
+            pre = look_back(st, tile, head);
+            if (lane == 0) publish(&st[tile], kFlagInc, pre + agg);
+        }
+        if (lane == 0) {
+            s_prefix = pre;
+            if (tile == ntiles - 1) {  // the grand totals
+                out_a[n] = pre.a + agg.a;
+                out_b[n] = pre.b + agg.b;
+            }
+        }
+    }
+    __syncthreads();
     // frame (i, wave, lane) follows rows < i (all waves) and waves < wave of row i
-    V2 run = partials[blockIdx.x];
+    V2 run = s_prefix;
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         V2 before{0, 0}, row{0, 0};
@@ -253,6 +296,14 @@ __global__ void __launch_bounds__(kBlock) scan_emit_kernel(Size size, uint32_t n
         }
         run = run + row;
     }
+}
+
+// Zeroes the workspace head and the scan's tile states (one launch; a memset
+// node replayed in a captured graph was seen writing garbage, kmws_common.hpp).
+__global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict__ p, uint64_t words)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
+        p[i] = 0;
 }
 
 // Dword I of the 8-dword window lo||hi (I fixed at compile time).
@@ -1133,7 +1184,7 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 // ------------------------------ host launchers ------------------------------
 struct CopyWs {
     WsHead* head;
-    V2* partials;
+    ScanState* states;  // right after the head: one zeroing launch covers both
     uint64_t* ubase;
     UnitRec* rec;
     u32x4* edge;
@@ -1163,7 +1214,7 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     char* p = static_cast<char*>(ws);
     c.head = reinterpret_cast<WsHead*>(p);
     p += sizeof(WsHead);
-    c.partials = reinterpret_cast<V2*>(p);
+    c.states = reinterpret_cast<ScanState*>(p);
     p += r16((n_scan_blocks(n) + 1) * sizeof(V2));
     c.ubase = reinterpret_cast<uint64_t*>(p);
     p += r16(((uint64_t)n + 1) * 8);
@@ -1174,20 +1225,24 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     return true;
 }
 
-// Region offsets -> out (n+1 entries), unit slot bases -> c.ubase (n+1 entries).
+// Region offsets -> out (n+1 entries), unit slot bases -> c.ubase (n+1 entries);
+// also zeroes the workspace head (status, ticket) first.  Two launches.
 template <class Size>
 static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s, u32x4* hdr = nullptr,
                                uint8_t* hl_out = nullptr)
 {
     const uint32_t nb = (uint32_t)n_scan_blocks(n);
     if (nb == 0) {
+        if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
         if (launch_zero(out, sizeof(uint64_t), s) != KMWS_OK) return KMWS_ERR_FAILED;
         return launch_zero(c.ubase, sizeof(uint64_t), s);
     }
-    hipLaunchKernelGGL(scan_reduce_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kBlock), 0, s, c.partials, nb, out + n, c.ubase + n);
-    hipLaunchKernelGGL(scan_emit_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, c.partials, out, c.ubase, hdr,
-                       hl_out);
+    const uint64_t words = (sizeof(WsHead) + (uint64_t)nb * sizeof(ScanState)) / 8;
+    const uint64_t zb = (words + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint64_t*>(c.head), words);
+    hipLaunchKernelGGL(scan_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, nb, c.states, c.head, out, c.ubase,
+                       hdr, hl_out);
     return hip_status(hipGetLastError());
 }
 
@@ -1321,7 +1376,6 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     kmws_status st = launch_scan(WireSize{descs, flags}, n, wire_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<true>(src, dst, dst_cap, wire_off, descs, flags, n, c, s);
@@ -1337,13 +1391,12 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c, s);
     if (st != KMWS_OK || n == 0) return st;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
 
-// scan partials + scratch unit bases after the status word (the scan's second
+// scan tile states + scratch unit bases after the status word (the scan's second
 // quantity is not needed here but costs nothing)
 size_t kmws_pack_headers_workspace_size(uint32_t n)
 {
@@ -1363,12 +1416,11 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
         char* p = static_cast<char*>(workspace);
         CopyWs c;
         c.head = reinterpret_cast<WsHead*>(p);
-        c.partials = reinterpret_cast<V2*>(p + sizeof(WsHead));
+        c.states = reinterpret_cast<ScanState*>(p + sizeof(WsHead));
         c.ubase = reinterpret_cast<uint64_t*>(p + sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)));
         c.rec = nullptr;
         c.edge = nullptr;
-        if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        // the scan's emit pass writes the header slots too
+        // the scan writes the header slots too
         return launch_scan(WireSize{descs, flags}, n, wire_off, c, s, reinterpret_cast<u32x4*>(hdr), hl_out);
     }
     if (n == 0) return KMWS_OK;

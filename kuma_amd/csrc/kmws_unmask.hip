@@ -29,16 +29,19 @@
 
 namespace kmws {
 
-// Payload store of a tile word: non-temporal (streams past the L2; the
-// default) or temporal (NT = false: the line stays in L2 and is written back
-// on eviction).  Which one streams faster depends on the batch's layout: on an
-// aligned arena temporal stores ran +0.3-1.0 points, on a packed wire image
-// they lost 1.6-7 (profiles/r02bz_unmask_store_policy_ab.txt), so the policy
-// is part of the schedule the autotune times on the caller's batch.
-template <bool NT>
-__device__ __forceinline__ void store_word(const u32x4& val, u32x4* p)
+// Payload store of a tile word: non-temporal (streams past the L2) or temporal
+// (the line stays in L2 and is written back on eviction).  Which one streams
+// faster depends on the batch's layout: on an aligned arena temporal stores ran
+// +0.3-1.0 points, on a packed wire image they lost 1.6-7
+// (profiles/r02bz_unmask_store_policy_ab.txt), so the policy is part of the
+// schedule.  `nt` is block-uniform (the apply grid's store policy resolved
+// against the plan's layout flag): a scalar branch around each store, ONE code
+// path -- two instantiations of the tile body behind a branch took the
+// uncapped kernel from 80 to 86 VGPRs, 6 to 5 waves per SIMD, and 4 KiB
+// fragments from 82 to 79 % (profiles/r03e_configs.jsonl).
+__device__ __forceinline__ void store_word(const u32x4& val, u32x4* p, bool nt)
 {
-    if constexpr (NT) __builtin_nontemporal_store(val, p);
+    if (nt) __builtin_nontemporal_store(val, p);
     else *p = val;
 }
 
@@ -98,12 +101,12 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint
 }
 
 // Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
-template <int V, bool FULL, bool TWO = false, bool NT = true>
+template <int V, bool FULL, bool TWO = false>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
                                             const kmws_desc* __restrict__ d, uint32_t n,
                                             const uint32_t* __restrict__ map, uint32_t tile, bool ok,
                                             const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key,
-                                            const u32x4* pre = nullptr)
+                                            const u32x4* pre = nullptr, bool nt = true)
 {
     using Cfg = UnmaskCfg<V>;
     const int tid = threadIdx.x;
@@ -121,7 +124,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-            if (ok) store_word<NT>(v[i] ^ r, reinterpret_cast<u32x4*>(base + a));
+            if (ok) store_word(v[i] ^ r, reinterpret_cast<u32x4*>(base + a), nt);
         }
         return;
     }
@@ -169,7 +172,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
             if (ok && (m[i].x | m[i].y | m[i].z | m[i].w) != 0u)
-                store_word<NT>(v[i] ^ m[i], reinterpret_cast<u32x4*>(base + a));
+                store_word(v[i] ^ m[i], reinterpret_cast<u32x4*>(base + a), nt);
         }
         return;
     }
@@ -236,7 +239,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
         const u32x4 mm = m[i];
         if (ok && (FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
-            store_word<NT>(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a));
+            store_word(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a), nt);
     }
 }
 
@@ -323,13 +326,8 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
         if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
         load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        const bool ok = head->status == 0;
-        if (nt_stores(head, store))
-            finish_tile<V, true, TWO, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key,
-                                            &pre);
-        else
-            finish_tile<V, true, TWO, false>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key,
-                                             &pre);
+        finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                  s_key, &pre, nt_stores(head, store));
         return;
     }
 #endif
@@ -337,11 +335,8 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     __builtin_amdgcn_sched_barrier(0);
     // the head (status, layout) is read after the payload loads: its latency
     // hides under theirs, and the store policy is a block-uniform branch
-    const bool ok = head->status == 0;
-    if (nt_stores(head, store))
-        finish_tile<V, true, TWO, true>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key);
-    else
-        finish_tile<V, true, TWO, false>(base, lo, lo + Cfg::kTile, d, n, map, tile, ok, v, s_off, s_end, s_key);
+    finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key,
+                              nullptr, nt_stores(head, store));
 }
 
 // Small host batches: the decoder's payloads of one socket read or one loop
@@ -547,8 +542,10 @@ static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n
 //
 // A schedule belongs to ONE batch: kmws_unmask_autotune / kmws_unmask_set_schedule
 // record it for (workspace, descs, n, span), and apply uses it only for that
-// batch; every other batch gets the default (grouped XCD runs, automatic store
-// policy).  The reference's handleDataMask (WSHandler.cpp:303-310) is stateless;
+// batch; every other batch gets the default: split 4 (the best or within 0.4
+// points of it on plain allocations of the aligned arena, the packed wire and
+// 4 KiB fragments, profiles/r03f_unmask_schedule_sweep_plain.jsonl), automatic
+// store policy.  The reference's handleDataMask (WSHandler.cpp:303-310) is stateless;
 // so is every batch that was not tuned.
 struct Split {
     uint32_t k, c, w;
@@ -556,7 +553,7 @@ struct Split {
 constexpr uint32_t kKindMask = 0xFFu;
 constexpr uint32_t kSchedTemporal = KMWS_SCHED_TEMPORAL_STORES;
 constexpr uint32_t kSchedNT = KMWS_SCHED_NT_STORES;
-constexpr uint32_t kDefaultSchedule = KMWS_SCHED_GROUPED_RUNS;
+constexpr uint32_t kDefaultSchedule = KMWS_SCHED_SPLIT4;
 
 static bool split_of(uint32_t kind, Split* sp)
 {

@@ -52,6 +52,7 @@ BENCH_EXPORTS = [
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
 SCHED_GROUPED_RUNS, SCHED_IN_ORDER, SCHED_SPLIT2, SCHED_SPLIT8, SCHED_XCD_RUNS, SCHED_SPLIT4 = 0, 1, 2, 3, 4, 5
 SCHED_KINDS = (0, 1, 2, 3, 4, 5)
+SCHED_DEFAULT = SCHED_SPLIT4  # what kmws_unmask_apply uses for a batch nobody tuned
 SCHED_NT_STORES, SCHED_TEMPORAL_STORES = 1 << 29, 1 << 30
 
 

@@ -229,8 +229,8 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     assert _valid_schedule(choice) and choice & (3 << 29)  # the autotune times forced store policies
     assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == choice
     ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
-    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS  # other batches: default
-    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.SCHED_GROUPED_RUNS  # other span
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_DEFAULT  # other batches: default
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.SCHED_DEFAULT  # other span
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
@@ -238,7 +238,7 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     torch.cuda.synchronize()
     assert ws.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
     kmws.unmask_set_schedule(ws, d_desc, len(buf), -1)  # forget: back to the default
-    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == kmws.SCHED_DEFAULT
 
 
 def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
@@ -264,7 +264,7 @@ def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
     buf, wd = layout("packed_wire", rng)
     d_buf, d_desc = _to_dev(torch, buf, wd)
     ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
-    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_GROUPED_RUNS
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_DEFAULT
     want = buf.copy()
     orc.unmask_batch(want, wd)
     kmws.unmask_batch(d_buf, d_desc, ws2, len(buf))
