@@ -561,7 +561,7 @@ def main():
         base_all = torch.empty(span, dtype=torch.uint8, device=dev)
 
     stream = torch.cuda.current_stream()
-    schedule = a.schedule if a.schedule >= 0 else kmws.SCHED_DEFAULT
+    schedule = a.schedule if a.schedule >= 0 else kmws.sched_default(span, n)
     elapsed, ev_ms, launches, alg_total, mismatches, st, done = 0.0, 0.0, 0, 0, 0, 0, 0
     ranges = []
     for j, (b_lo, b_hi) in enumerate(batches):

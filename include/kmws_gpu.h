@@ -244,15 +244,17 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
 /* Unmask schedules.  The apply grid is one block per 16 KiB tile; a schedule
  * says which tiles the resident blocks stream at once and how the payload is
  * stored.  Placement kind (low byte): */
-#define KMWS_SCHED_GROUPED_RUNS 0   /* XCDs in 2 groups, runs of 16 tiles in each group's half */
+#define KMWS_SCHED_GROUPED_RUNS 0   /* XCDs in 2 groups, runs of 16 tiles in each group's half
+                                       (the default below a mean frame region of 16 KiB) */
 #define KMWS_SCHED_IN_ORDER     1   /* tile = block */
 #define KMWS_SCHED_SPLIT2       2   /* blocks dealt over 2 far-apart parts of the span */
 #define KMWS_SCHED_SPLIT8       3   /* ... over 8 parts */
 #define KMWS_SCHED_XCD_RUNS     4   /* runs of 16 tiles per XCD */
-#define KMWS_SCHED_SPLIT4       5   /* ... over 4 parts (the default) */
-/* Store policy (at most one bit; neither = automatic: temporal stores when every
- * frame of the batch starts on a 16 KiB tile boundary -- the plan records the
- * layout -- non-temporal otherwise, e.g. for a packed wire image). */
+#define KMWS_SCHED_SPLIT4       5   /* ... over 4 parts (the default from a 16 KiB mean region) */
+/* Store policy of the payload: non-temporal by default (neither bit, or
+ * KMWS_SCHED_NT_STORES); KMWS_SCHED_TEMPORAL_STORES keeps the lines in L2
+ * (written back on eviction) -- slower on plain allocations of every layout
+ * measured, a candidate the autotune times.  At most one bit. */
 #define KMWS_SCHED_NT_STORES       (1 << 29)
 #define KMWS_SCHED_TEMPORAL_STORES (1 << 30)
 
@@ -261,8 +263,8 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
  * applied twice leaves the payload unchanged), times them with events on
  * `stream` (synchronizes) and records the fastest for this batch -- the tuple
  * (workspace, descs, n, span) -- where kmws_unmask_apply / kmws_unmask_batch
- * find it.  Every other batch keeps the default schedule (split 4,
- * automatic stores): no device-global state.  Returns the chosen schedule code
+ * find it.  Every other batch keeps the default schedule (split 4 or grouped
+ * runs by mean region, non-temporal stores): no device-global state.  Returns the chosen schedule code
  * or a negative status. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
@@ -303,9 +305,10 @@ size_t kmws_pack_headers_workspace_size(uint32_t n);
  * WSHandler::encodeFrameHeader (WSHandler.cpp:46-106) of {flags[i],
  * descs[i].len, descs[i].key}, is written to the 16-byte slot hdr + 16 i (its
  * hdr_len[i] = 2..14 bytes first, the rest of the slot zero).  The payloads are
- * not touched: mask them in place with kmws_unmask_batch on the same
- * descriptors (XOR is its own inverse), as sendWsFrame masks the caller's
- * buffer (:388).  wire_off (n+1 entries, may be NULL) receives the offsets the
+ * not touched: mask them in place with kmws_unmask_batch (XOR is its own
+ * inverse), as sendWsFrame masks the caller's buffer (:388), on descriptors
+ * whose key is 0 for every frame whose flags clear KMWS_FLAG_MASK (the header
+ * then says unmasked; a nonzero key there would still be applied).  wire_off (n+1 entries, may be NULL) receives the offsets the
  * frames would have back to back on the wire (exclusive scan of header +
  * payload bytes) and the total in wire_off[n].  hdr 16-B aligned. */
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,

@@ -12,21 +12,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
 
-// First 16 bytes of every workspace: status word and layout flags (+ pad),
-// zeroed by launch_zero (a kernel, not a memset node: see below) at the start
-// of each batch call.
+// First 16 bytes of every workspace: status word (+ the scan's ticket
+// counter), zeroed by a kernel (not a memset node: see launch_zero) at the
+// start of each batch call.
 struct WsHead {
     uint32_t status;
-    uint32_t layout;  // kLayout* bits, written by the unmask plan
-    uint32_t ticket;  // tile tickets of the single-pass scan (kmws_pack.hip)
-    uint32_t pad;
+    uint32_t pad0;
+    uint32_t ticket;  // tile tickets of the single-pass scans (kmws_pack.hip)
+    uint32_t pad1;
 };
 constexpr uint32_t kStatusBadDesc = 1u;
 constexpr uint32_t kStatusBadHeader = 2u;
-// A frame of the batch does not start on a tile boundary (a packed wire image,
-// small frames): the unmask's automatic store policy then keeps non-temporal
-// payload stores.
-constexpr uint32_t kLayoutUnaligned = 1u;
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {

@@ -180,40 +180,70 @@ __device__ __forceinline__ void publish(ScanState* st, uint64_t flag, V2 v)
     st_agent(&st->b, flag << 62 | (v.b & kValMask));
 }
 
-// Wave 0 of tile `tile`: the exclusive prefix of the tiles before it.  Lane l
-// looks at tile j - l of a 64-tile window; the window's tiles up to and
-// including the nearest one with an inclusive prefix contribute (nonexistent
-// tiles below 0 count as an inclusive zero); without one the window's
-// aggregates are summed and the window moves 64 tiles back.
+// Wave 0 of tile `tile`: the exclusive prefix of the tiles before it.  The
+// wave looks at a window of 256 tiles below j = tile - 1 at once (lane l, item
+// k: tile j - l - 64 k; four independent loads per lane); the window's tiles up
+// to and including the nearest one with an inclusive prefix contribute
+// (nonexistent tiles below 0 count as an inclusive zero); without one the
+// window's aggregates are summed and the window moves 256 tiles back.  With
+// every tile of a grid starting at once, the prefixes propagate through chains
+// of aggregates, so a window of 64 made tile 1,000 wait for ~16 dependent
+// rounds of loads; 256 makes it 4.
+constexpr int kLookItems = 4;
 __device__ V2 look_back(const ScanState* __restrict__ st, uint32_t tile, WsHead* __restrict__ head)
 {
     const int lane = threadIdx.x & 63;
     V2 ex{0, 0};
-    for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64) {
-        const int64_t p = j - lane;
-        uint64_t kind = kFlagInc, va = 0, vb = 0;
-        if (p >= 0) {
-            for (uint32_t spins = 0;; ++spins) {
+    for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64 * kLookItems) {
+        uint32_t flag[kLookItems];  // 0: not published yet, kFlagAgg, kFlagInc (tiles below 0: an inclusive zero)
+        uint64_t va[kLookItems], vb[kLookItems];
+#pragma unroll
+        for (int k = 0; k < kLookItems; ++k) {
+            flag[k] = j - lane - 64 * k < 0 ? (uint32_t)kFlagInc : 0u;
+            va[k] = vb[k] = 0;
+        }
+        for (uint32_t spins = 0;; ++spins) {
+            bool done = true;
+#pragma unroll
+            for (int k = 0; k < kLookItems; ++k) {
+                if (flag[k] != 0) continue;
+                const int64_t p = j - lane - 64 * k;
                 const uint64_t A = ld_agent(&st[p].a), B = ld_agent(&st[p].b);
                 if ((A >> 62) != 0 && (A >> 62) == (B >> 62)) {
-                    kind = A >> 62;
-                    va = A & kValMask;
-                    vb = B & kValMask;
-                    break;
+                    flag[k] = (uint32_t)(A >> 62);
+                    va[k] = A & kValMask;
+                    vb[k] = B & kValMask;
+                } else {
+                    done = false;
                 }
-                if (spins >= kSpinLimit) {  // cannot happen: every ticketed tile publishes
-                    atomicOr(&head->status, kStatusBadDesc);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+            }
+            if (__all(done)) break;
+            if (spins >= kSpinLimit) {  // cannot happen: every ticketed tile publishes
+                atomicOr(&head->status, kStatusBadDesc);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        // the nearest inclusive tile in distance order (item k, then lane)
+        int first_k = kLookItems, first_l = 64;
+#pragma unroll
+        for (int k = kLookItems - 1; k >= 0; --k) {
+            const uint64_t inc = __ballot(flag[k] == (uint32_t)kFlagInc);
+            if (inc) {
+                first_k = k;
+                first_l = __ffsll((unsigned long long)inc) - 1;
             }
         }
-        const uint64_t inc = __ballot(kind == kFlagInc);
-        const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
-        const bool take = lane <= first;
-        ex.a += wave_sum(take ? va : 0);
-        ex.b += wave_sum(take ? vb : 0);
-        if (inc) break;
+        V2 part{0, 0};
+#pragma unroll
+        for (int k = 0; k < kLookItems; ++k) {
+            const bool take = k < first_k || (k == first_k && lane <= first_l);
+            part.a += take ? va[k] : 0;
+            part.b += take ? vb[k] : 0;
+        }
+        ex.a += wave_sum(part.a);
+        ex.b += wave_sum(part.b);
+        if (first_k < kLookItems) break;
     }
     return ex;
 }
@@ -235,16 +265,21 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(Size size, uint32_t n, uin
     const uint32_t tile = s_tile;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t base = (uint64_t)tile * kScanTile + threadIdx.x;
-    V2 ex[kScanItems];
+    // 1. row totals per wave (values not kept: the emit pass re-reads the frames,
+    //    cache-hot, so no per-frame state lives in registers across the look-back)
+    V2 v[kScanItems];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         const uint64_t f = base + (uint64_t)i * kBlock;
-        const V2 v = f < n ? size((uint32_t)f) : V2{0, 0};
-        const V2 inc{wave_incl_scan(v.a), wave_incl_scan(v.b)};
-        ex[i] = V2{inc.a - v.a, inc.b - v.b};
-        if (lane == 63) s_row[i][wave] = inc;
+        v[i] = f < n ? size((uint32_t)f) : V2{0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const V2 t{wave_sum(v[i].a), wave_sum(v[i].b)};
+        if (lane == 0) s_row[i][wave] = t;
     }
     __syncthreads();
+    // 2. the tile's aggregate, published; its prefix by look-back (wave 0)
     if (wave == 0) {
         V2 agg{0, 0};
 #pragma unroll
@@ -263,12 +298,12 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(Size size, uint32_t n, uin
             s_prefix = pre;
             if (tile == ntiles - 1) {  // the grand totals
                 out_a[n] = pre.a + agg.a;
-                out_b[n] = pre.b + agg.b;
+                if (out_b) out_b[n] = pre.b + agg.b;
             }
         }
     }
     __syncthreads();
-    // frame (i, wave, lane) follows rows < i (all waves) and waves < wave of row i
+    // 3. emit: frame (i, wave, lane) follows rows < i (all waves) and waves < wave of row i
     V2 run = s_prefix;
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
@@ -280,17 +315,19 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(Size size, uint32_t n, uin
             row = row + t;
         }
         const uint64_t f = base + (uint64_t)i * kBlock;
+        const V2 x = f < n ? size((uint32_t)f) : V2{0, 0};
+        const V2 inc{wave_incl_scan(x.a), wave_incl_scan(x.b)};
         if (f < n) {
-            out_a[f] = run.a + before.a + ex[i].a;
-            out_b[f] = run.b + before.b + ex[i].b;
+            out_a[f] = run.a + before.a + inc.a - x.a;
+            if (out_b) out_b[f] = run.b + before.b + inc.b - x.b;
             if constexpr (Size::kHeaders) {
                 if (hdr) {
-                    const kmws_desc x = size.d[f];
+                    const kmws_desc dx = size.d[f];
                     const uint32_t fl = size.flags[f];
                     uint64_t h0, h1;
-                    build_header(x.len, fl, x.key, h0, h1);
+                    build_header(dx.len, fl, dx.key, h0, h1);
                     hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                    if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
+                    if (hl_out) hl_out[f] = (uint8_t)hdr_len(dx.len, (fl >> 8) & 1u);
                 }
             }
         }
@@ -441,57 +478,56 @@ struct UnitRec {
 };
 static_assert(sizeof(UnitRec) == 32, "UnitRec is one s_load_dwordx8");
 
-// Geometry (and flags) of frames f, f+1, f+2 -- the frames a word starting in
+// Geometry of frame j given where its region starts (regions lie back to back:
+// frame j+1 starts where frame j's payload ends).
+template <bool HEADERS>
+__device__ __forceinline__ FrameGeom geom_at(const kmws_desc& x, uint32_t fl, uint64_t r0)
+{
+    const uint32_t mask = HEADERS ? (fl >> 8) & 1u : 1u;
+    FrameGeom g;
+    g.r0 = r0;
+    g.p0 = r0 + (HEADERS ? hdr_len(x.len, mask) : 0u);
+    g.r1 = g.p0 + x.len;
+    g.sdel = x.off - g.p0;
+    g.key = mask ? x.key : 0u;
+    g.len = x.len;
+    return g;
+}
+
+// Descriptors (and flags) of frames f, f+1, f+2 -- the frames a word starting in
 // frame f overlaps in all but tiny-frame batches -- loaded at once (indices
 // clamped instead of branches, so the loads issue together).
 constexpr int kPre = 3;
 template <bool HEADERS>
-__device__ __forceinline__ void load_geoms(uint32_t f, uint32_t n, FrameGeom (&g)[kPre], uint32_t (&fl)[kPre],
-                                           const uint64_t* __restrict__ start, const kmws_desc* __restrict__ d,
-                                           const uint16_t* __restrict__ flags)
+__device__ __forceinline__ void load_descs(uint32_t f, uint32_t n, kmws_desc (&x)[kPre], uint32_t (&fl)[kPre],
+                                           const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags)
 {
-    kmws_desc x[kPre];
-    uint64_t r0[kPre];
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) {  // every load first, then the arithmetic
-        const uint32_t j = f + i < n ? f + i : n - 1;
-        x[i] = d[j];
-        r0[i] = start[j];
-        fl[i] = HEADERS ? flags[j] : 0u;
-    }
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
-        const uint32_t mask = HEADERS ? (fl[i] >> 8) & 1u : 1u;
-        const uint32_t hl = HEADERS ? hdr_len(x[i].len, mask) : 0u;
-        g[i].r0 = f + i < n ? r0[i] : ~0ull;  // past the last frame: overlaps nothing
-        g[i].p0 = r0[i] + hl;
-        g[i].r1 = g[i].p0 + x[i].len;
-        g[i].sdel = x[i].off - g[i].p0;
-        g[i].key = mask ? x[i].key : 0u;
-        g[i].len = x[i].len;
+        const uint32_t j = f + i < n ? f + i : n - 1;
+        x[i] = d[j];
+        fl[i] = HEADERS ? flags[j] : 0u;
     }
 }
 
 // Output word [a, a + 16) composed byte by byte from every frame from f on that
 // overlaps it -- the rare word three or more regions reach into (frames shorter
-// than a word); few registers, one frame's geometry at a time.
+// than a word); few registers, one frame's geometry at a time (frame j+1's
+// region starts where frame j's ends).
 template <bool HEADERS>
 __device__ __attribute__((noinline)) u32x4 compose_word_bytes(uint64_t a, uint32_t f, uint32_t n,
-                                                              const uint8_t* __restrict__ src,
-                                                              const uint64_t* __restrict__ start,
-                                                              const kmws_desc* __restrict__ d,
+                                                              const uint8_t* __restrict__ src, FrameGeom h,
+                                                              uint32_t flj, const kmws_desc* __restrict__ d,
                                                               const uint16_t* __restrict__ flags)
 {
     u32x4 out = u32x4{0, 0, 0, 0};
     uint32_t j = f;
-    FrameGeom h = geom<HEADERS>(j, start, d, flags);
-    uint32_t flj = HEADERS ? flags[j] : 0u;
     for (uint32_t b = 0; b < 16; ++b) {
         const uint64_t x = a + b;
         while (x >= h.r1 && j + 1 < n) {
             ++j;
-            h = geom<HEADERS>(j, start, d, flags);
             flj = HEADERS ? flags[j] : 0u;
+            h = geom_at<HEADERS>(d[j], flj, h.r1);
         }
         if (x < h.r0 || x >= h.r1) continue;  // past the last region
         uint32_t v;
@@ -558,7 +594,13 @@ struct FrameUnits {
     uint32_t rk, units, head_f, nedge;
 };
 
-// Everything the copy waves need of 256 frames, one block:
+// Scan + everything the copy waves need of 256 frames, one block (one launch
+// for the whole batch, blocks in ticket order):
+//   the scan: the block's region sizes (header + payload) and unit-slot bounds
+//     scanned in LDS, the block's exclusive prefix by decoupled look-back
+//     (look_back), frame offsets -> start[f] and unit slot bases -> ubase[f]
+//     (start[n], ubase[n] = the totals, by the last block); frame f+1's region
+//     starts where frame f's ends, so a block needs no other block's offsets;
 //   edge words -- a frame's owned words outside its interior: q < head_f at
 //     olo + q, then the tail at ihi + (q - head_f) -- one thread per frame,
 //     into LDS, then written out over one contiguous run edge[F0 * kEdgeWords ...]
@@ -575,39 +617,90 @@ struct FrameUnits {
 // of frame f+1 from which every tail word funnels its payload bytes (window
 // indices clamped to f+1's payload; clamped words only feed bytes outside it,
 // which are masked off).  The rare word a third region reaches into (a frame
-// ending inside it) is composed byte by byte.  Also the capacity check (status
-// set if the output exceeds cap; nothing is written then).
+// ending inside it) is composed byte by byte.  Owned words past the end of the
+// output (the last frame's last granule) are composed as zero and never stored
+// by the copy waves, which clip at the total.  Capacity: a block whose regions
+// end past `cap` sets the status and writes no record or edge word (its slots
+// could lie past the workspace); the copy waves then write nothing.
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
-                                                          const uint64_t* __restrict__ start,
-                                                          const uint64_t* __restrict__ ubase,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags, uint32_t n,
-                                                          uint64_t cap, UnitRec* __restrict__ rec,
-                                                          u32x4* __restrict__ edge, WsHead* __restrict__ head,
-                                                          uint64_t f_lo, uint64_t f_hi)
+__global__ void __launch_bounds__(kBlock) scan_prologue_kernel(const uint8_t* __restrict__ src,
+                                                               const kmws_desc* __restrict__ d,
+                                                               const uint16_t* __restrict__ flags, uint32_t n,
+                                                               uint32_t ntiles, uint64_t cap,
+                                                               ScanState* __restrict__ st, WsHead* __restrict__ head,
+                                                               uint64_t* __restrict__ start,
+                                                               uint64_t* __restrict__ ubase, UnitRec* __restrict__ rec,
+                                                               u32x4* __restrict__ edge)
 {
     __shared__ FrameUnits s_fu[kBlock];
     __shared__ uint32_t s_ub[kBlock + 1];
     __shared__ u32x4 s_edge[kBlock * kEdgeWords];
     __shared__ uint8_t s_ne[kBlock];  // live edge words per frame
-    const uint64_t F0 = f_lo + (uint64_t)blockIdx.x * kBlock;
-    const uint32_t nf = f_hi - F0 < (uint64_t)kBlock ? (uint32_t)(f_hi - F0) : (uint32_t)kBlock;
+    __shared__ V2 s_wave[kBlock / 64];
+    __shared__ V2 s_pre;
+    __shared__ uint32_t s_tile;
     const uint32_t t = threadIdx.x;
-    // total, slot bases and the three frames' geometry: one latency level
-    const uint64_t total = start[n];
-    const uint64_t S0 = ubase[F0];
+    const int lane = t & 63, wave = t >> 6;
+    if (t == 0) s_tile = atomicAdd(&head->ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t F0 = (uint64_t)tile * kBlock;
+    const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
     const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
-    const uint64_t uf = ubase[f], uend = ubase[F0 + nf];
-    FrameGeom g[kPre];
+    kmws_desc x[kPre];
     uint32_t fl[kPre];
-    load_geoms<HEADERS>(f, n, g, fl, start, d, flags);
-    if (total > cap) {  // records would not fit the workspace; the copy waves see the status (block-uniform)
-        if (F0 == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
+    load_descs<HEADERS>(f, n, x, fl, d, flags);
+    // this frame's region and unit-slot bound, scanned over the block
+    const uint32_t hl0 = HEADERS ? hdr_len(x[0].len, (fl[0] >> 8) & 1u) : 0u;
+    const uint64_t R = t < nf ? (uint64_t)hl0 + x[0].len : 0, U = unit_bound(R);
+    const uint64_t incR = wave_incl_scan(R), incU = wave_incl_scan(U);
+    if (lane == 63) s_wave[wave] = V2{incR, incU};
+    __syncthreads();
+    V2 before{0, 0}, agg{0, 0};
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const V2 v = s_wave[w];
+        if (w < wave) before = before + v;
+        agg = agg + v;
+    }
+    if (wave == 0) {
+        V2 pre{0, 0};
+        if (tile == 0) {
+            if (lane == 0) publish(&st[0], kFlagInc, agg);
+        } else {
+            if (lane == 0) publish(&st[tile], kFlagAgg, agg);
+            pre = look_back(st, tile, head);
+            if (lane == 0) publish(&st[tile], kFlagInc, pre + agg);
+        }
+        if (lane == 0) {
+            s_pre = pre;
+            if (tile == ntiles - 1) {  // the grand totals
+                start[n] = pre.a + agg.a;
+                ubase[n] = pre.b + agg.b;
+            }
+        }
+    }
+    __syncthreads();
+    const V2 pre = s_pre;
+    const uint64_t r0 = pre.a + before.a + incR - R, uf = pre.b + before.b + incU - U;
+    if (t < nf) {
+        start[f] = r0;
+        ubase[f] = uf;
+    }
+    if (pre.a + agg.a > cap) {  // block-uniform: records would not fit the workspace; the copy waves see the status
+        if (t == 0) atomicOr(&head->status, kStatusBadDesc);
         return;
     }
+    const uint64_t S0 = pre.b, uend = pre.b + agg.b;
+    FrameGeom g[kPre];
+    g[0] = geom_at<HEADERS>(x[0], fl[0], r0);
+#pragma unroll
+    for (int i = 1; i < kPre; ++i) {
+        g[i] = geom_at<HEADERS>(x[i], fl[i], g[i - 1].r1);
+        if ((uint64_t)f + i >= n) g[i].r0 = ~0ull;  // past the last frame: overlaps nothing
+    }
     if (t < nf) {
-        const FrameWords w = frame_words(g[0], (total + 15) >> 4);
+        const FrameWords w = frame_words(g[0], ~0ull >> 4);  // unclipped: the copy waves clip at the total
         uint32_t head_f = (uint32_t)(w.ilo - w.olo);
         uint32_t nedge = head_f + (uint32_t)(w.ohi - w.ihi);
         if (nedge > (uint32_t)kEdgeWords || w.olo - w.b0 >= kUnitAlign) {  // cannot happen
@@ -691,7 +784,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         for (int q = 0; third != 0; ++q, third >>= 1) {
             if (third & 1u) {
                 const uint64_t a = 16u * ((uint32_t)q < head_f ? w.olo + q : w.ihi + (q - head_f));
-                my[q] = compose_word_bytes<HEADERS>(a, f, n, src, start, d, flags);
+                my[q] = compose_word_bytes<HEADERS>(a, f, n, src, g[0], fl[0], d, flags);
             }
         }
     }
@@ -891,9 +984,7 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
                                                       const UnitRec* __restrict__ rec,
                                                       const u32x4* __restrict__ edge,
                                                       const WsHead* __restrict__ head, uint64_t unit_base,
-                                                      uint32_t split, const uint64_t* __restrict__ chunk_lo,
-                                                      const uint64_t* __restrict__ chunk_hi, uint64_t stride,
-                                                      uint64_t slots)
+                                                      uint32_t split)
 {
     const int lane = threadIdx.x & 63;
     // wave id through readfirstlane: provably uniform, so the record is one scalar load
@@ -909,47 +1000,24 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
         const uint32_t q = gridDim.x / split;
         if (b < q * split) b = (b % split) * q + b / split;
     }
-    if (chunk_lo == nullptr) {  // the whole batch in one grid (the default)
-        const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
-        // record, slot count, status and total are independent scalar loads (one
-        // latency level); slots past the count lie inside the workspace and are ignored
-        const UnitRec r = rec[u];
-        const uint64_t total_units = ubase[n];
-        const uint32_t st = head->status;
-        const uint64_t total = start[n];
-        // no early exit between these loads and their uses (the compiler would sink
-        // the record load below the count's wait): an out-of-range wave owns no words
-        const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
-        // keep every field's load above the exit (one wait for all of them)
-        asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
-        if (x.khi == 0) return;  // wave-uniform, after the record's wait
-        // Every load is issued before the first store (vmcnt also counts stores, so
-        // a load issued after a store would make its wait cover that store too).
-        UnitRegs R;
-        unit_issue(x, lane, src, edge, R);
-        unit_finish(x, lane, dst, total, R);
-        return;
-    }
-    // One chunk of the pack pipeline: units [*chunk_lo, *chunk_hi) (the unit
-    // bases of the chunk's first frame and of the next chunk's), grid-strided
-    // by `stride` units since the host cannot size the grid to the chunk.  A
-    // batch whose records were not written (status set: the wire exceeds
-    // dst_cap, so the unit bases may run past the `slots` records the
-    // workspace holds) reads no record at all; u_hi is clamped to `slots` too.
+    const uint64_t u = unit_base + (uint64_t)b * (kBlock / 64) + wave;
+    // record, slot count, status and total are independent scalar loads (one
+    // latency level); slots past the count lie inside the workspace and are ignored
+    const UnitRec r = rec[u];
+    const uint64_t total_units = ubase[n];
     const uint32_t st = head->status;
-    if (st != 0) return;
-    const uint64_t u_lo = *chunk_lo, u_hi = *chunk_hi < slots ? *chunk_hi : slots;
     const uint64_t total = start[n];
-    for (uint64_t u = u_lo + unit_base + (uint64_t)b * (kBlock / 64) + wave; u < u_hi; u += stride) {
-        const UnitRec r = rec[u];
-        const UnitInfo x = decode_unit(r, true, src);
-        asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
-        if (x.khi != 0) {
-            UnitRegs R;
-            unit_issue(x, lane, src, edge, R);
-            unit_finish(x, lane, dst, total, R);
-        }
-    }
+    // no early exit between these loads and their uses (the compiler would sink
+    // the record load below the count's wait): an out-of-range wave owns no words
+    const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
+    // keep every field's load above the exit (one wait for all of them)
+    asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
+    if (x.khi == 0) return;  // wave-uniform, after the record's wait
+    // Every load is issued before the first store (vmcnt also counts stores, so
+    // a load issued after a store would make its wait cover that store too).
+    UnitRegs R;
+    unit_issue(x, lane, src, edge, R);
+    unit_finish(x, lane, dst, total, R);
 }
 
 // ------------------------------ header unpack / validate ------------------------------
@@ -1191,6 +1259,8 @@ struct CopyWs {
 };
 
 static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
+// tiles of the fused scan + prologue (256 frames each): one tile state each
+static uint64_t n_copy_tiles(uint32_t n) { return ((uint64_t)n + kBlock - 1) / kBlock; }
 // sum of unit_bound(R_f) <= total / (16 U) + n (1 + 63 / U) (and total <= cap)
 // (rounded up to whole blocks: every wave of the copy grid reads its record)
 static uint64_t max_units(uint32_t n, uint64_t cap)
@@ -1204,7 +1274,7 @@ static uint64_t r256(uint64_t x) { return (x + 255) & ~255ull; }
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    return r256(sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8)) +
+    return r256(sizeof(WsHead) + r16((n_copy_tiles(n) + 1) * sizeof(ScanState)) + r16(((uint64_t)n + 1) * 8)) +
            r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
 }
 
@@ -1215,7 +1285,7 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     c.head = reinterpret_cast<WsHead*>(p);
     p += sizeof(WsHead);
     c.states = reinterpret_cast<ScanState*>(p);
-    p += r16((n_scan_blocks(n) + 1) * sizeof(V2));
+    p += r16((n_copy_tiles(n) + 1) * sizeof(ScanState));
     c.ubase = reinterpret_cast<uint64_t*>(p);
     p += r16(((uint64_t)n + 1) * 8);
     p = static_cast<char*>(ws) + r256(p - static_cast<char*>(ws));  // edge words and records on whole lines
@@ -1225,8 +1295,9 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     return true;
 }
 
-// Region offsets -> out (n+1 entries), unit slot bases -> c.ubase (n+1 entries);
-// also zeroes the workspace head (status, ticket) first.  Two launches.
+// kmws_pack_headers: wire offsets -> out (n+1 entries) and the header slots;
+// also zeroes the workspace head (status, ticket) and tile states first.  Two
+// launches.
 template <class Size>
 static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s, u32x4* hdr = nullptr,
                                uint8_t* hl_out = nullptr)
@@ -1234,126 +1305,50 @@ static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, 
     const uint32_t nb = (uint32_t)n_scan_blocks(n);
     if (nb == 0) {
         if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        if (launch_zero(out, sizeof(uint64_t), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        return launch_zero(c.ubase, sizeof(uint64_t), s);
+        return launch_zero(out, sizeof(uint64_t), s);
     }
     const uint64_t words = (sizeof(WsHead) + (uint64_t)nb * sizeof(ScanState)) / 8;
     const uint64_t zb = (words + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
                        reinterpret_cast<uint64_t*>(c.head), words);
-    hipLaunchKernelGGL(scan_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, nb, c.states, c.head, out, c.ubase,
-                       hdr, hl_out);
+    // (the unit-slot bases, the scan's second quantity, are not needed here: not written)
+    hipLaunchKernelGGL(scan_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, nb, c.states, c.head, out,
+                       (uint64_t*)nullptr, hdr, hl_out);
     return hip_status(hipGetLastError());
 }
 
-// Side stream + events of the pack pipeline, one set per (host thread, device):
-// kmws calls come from each event loop's own thread, on that loop's stream.
-constexpr uint32_t kMaxPackChunks = 8;
-constexpr int kPackDevices = 16;
-struct PackSide {
-    hipStream_t ss;
-    hipEvent_t fork, ev[kMaxPackChunks];
-    bool ready;
-};
-static PackSide* pack_side()
-{
-    thread_local PackSide side[kPackDevices];  // created on first use, kept for the thread's life
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kPackDevices) return nullptr;
-    PackSide& p = side[dev];
-    if (!p.ready) {
-        if (hipStreamCreateWithFlags(&p.ss, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&p.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-        for (uint32_t j = 0; j < kMaxPackChunks; ++j)
-            if (hipEventCreateWithFlags(&p.ev[j], hipEventDisableTiming) != hipSuccess) return nullptr;
-        p.ready = true;
-    }
-    return &p;
-}
-
-// Frame chunks of the pack pipeline (1 = one record/edge grid, then one copy
-// grid).  KMWS_PACK_CHUNKS overrides it (tuning).
-static uint32_t pack_chunks(uint32_t n)
-{
-    static const uint32_t k = [] {
-        const char* e = getenv("KMWS_PACK_CHUNKS");
-        const int v = e ? atoi(e) : 1;
-        return v < 1 ? 1u : (v > (int)kMaxPackChunks ? kMaxPackChunks : (uint32_t)v);
-    }();
-    return (uint64_t)n >= (uint64_t)k * kBlock ? k : 1u;  // at least one record block per chunk
-}
-
+// Encode / gather: zero the head and the scan's tile states, the fused scan +
+// prologue (offsets, unit slot bases, edge words, unit records), the copy grid.
+// Three launches, stream-ordered, nothing on the host in between.
 template <bool HEADERS>
-static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, const uint64_t* start,
-                               const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
+static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
+                               const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
-    const uint32_t fb = (n + kBlock - 1) / kBlock;
-    constexpr uint64_t kMaxFrames = (1ull << 31) - kBlock;  // stay below 2^31 work-items per launch
-    auto prologue = [&](uint64_t F0, uint64_t F1, hipStream_t st) {  // records + edge words of frames [F0, F1)
-        for (uint64_t f0 = F0; f0 < F1; f0 += kMaxFrames) {
-            const uint64_t f1 = F1 - f0 < kMaxFrames ? F1 : f0 + kMaxFrames;
-            hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)((f1 - f0 + kBlock - 1) / kBlock)), dim3(kBlock),
-                               0, st, src, start, c.ubase, d, flags, n, cap, c.rec, c.edge, c.head, f0, f1);
-        }
-    };
+    if (n == 0) {
+        if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+        if (launch_zero(start, sizeof(uint64_t), s) != KMWS_OK) return KMWS_ERR_FAILED;
+        return launch_zero(c.ubase, sizeof(uint64_t), s);
+    }
+    const uint32_t nt = (n + kBlock - 1) / kBlock;  // scan + prologue tiles (256 frames)
+    const uint64_t words = (sizeof(WsHead) + (uint64_t)nt * sizeof(ScanState)) / 8;
+    const uint64_t zb = (words + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint64_t*>(c.head), words);
+    hipLaunchKernelGGL(scan_prologue_kernel<HEADERS>, dim3(nt), dim3(kBlock), 0, s, src, d, flags, n, nt, cap,
+                       c.states, c.head, start, c.ubase, c.rec, c.edge);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
     // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
     // batches of small frames need every wave slot to hide their per-unit
     // latency.  cap / n bounds the mean region size from above.
-    // KMWS_COPY_LDS_PAD overrides the LDS bytes per block (tuning).
-    static const int lds_env = [] {
-        const char* e = getenv("KMWS_COPY_LDS_PAD");
-        return e ? atoi(e) : -1;
-    }();
-    const unsigned lds_pad = lds_env >= 0 ? (unsigned)lds_env : (cap / n >= 16384 ? 32768u : 0u);
-    // Blocks dealt over kCopySplit far-apart parts of the output (as the unmask
-    // schedule); KMWS_COPY_SPLIT overrides it (tuning).
-    static const uint32_t split = [] {
-        const char* e = getenv("KMWS_COPY_SPLIT");
-        const int v = e ? atoi(e) : -1;
-        return v >= 1 ? (uint32_t)v : kCopySplit;
-    }();
+    const unsigned lds_pad = cap / n >= 16384 ? 32768u : 0u;
     const uint64_t units = max_units(n, cap);  // upper bound; surplus waves exit at once
     constexpr uint64_t kWavesPerBlock = kBlock / 64;
     constexpr uint64_t kMaxUnitsPerLaunch = ((1ull << 32) / kBlock / 2) * kWavesPerBlock;
-    const uint32_t K = pack_chunks(n);
-    if (K == 1) {
-        prologue(0, n, s);
-        for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
-            const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
-            hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                               dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head,
-                               u0, split, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)0, units);
-        }
-        return hip_status(hipGetLastError());
-    }
-    // Pipeline: the prologue grids of the K frame chunks run back to back on a
-    // side stream while the copy grid of chunk j (caller's stream) waits only for
-    // chunk j's prologue, so all but the first chunk's prologue hides under copies.
-    // Fork and join are events, so the call stays stream-ordered and capturable.
-    // A unit reads only its own frame's record and edge words, each written by
-    // that frame's prologue thread: no grid writes what a running copy grid reads.
-    PackSide* ps = pack_side();
-    if (!ps) return KMWS_ERR_FAILED;
-    if (hipEventRecord(ps->fork, s) != hipSuccess || hipStreamWaitEvent(ps->ss, ps->fork, 0) != hipSuccess)
-        return KMWS_ERR_FAILED;
-    auto chunk_frame = [&](uint32_t j) -> uint64_t {  // first frame of chunk j (j = K: n)
-        const uint64_t f = (uint64_t)kBlock * ((uint64_t)fb * j / K);
-        return f < n ? f : n;
-    };
-    for (uint32_t j = 0; j < K; ++j) {
-        prologue(chunk_frame(j), chunk_frame(j + 1), ps->ss);
-        if (hipEventRecord(ps->ev[j], ps->ss) != hipSuccess) return KMWS_ERR_FAILED;
-    }
-    uint64_t gw = (units + K - 1) / K;  // waves per chunk grid (equal chunks: one unit each)
-    gw = (gw + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
-    gw = gw < kMaxUnitsPerLaunch ? gw : kMaxUnitsPerLaunch;
-    for (uint32_t j = 0; j < K; ++j) {
-        const uint64_t F0 = chunk_frame(j), F1 = chunk_frame(j + 1);
-        if (hipStreamWaitEvent(s, ps->ev[j], 0) != hipSuccess) return KMWS_ERR_FAILED;
-        hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)(gw / kWavesPerBlock)), dim3(kBlock), lds_pad, s, src,
-                           dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, (uint64_t)0, split,
-                           (const uint64_t*)(c.ubase + F0), (const uint64_t*)(c.ubase + F1), gw, units);
+    for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
+        const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
+        hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0,
+                           kCopySplit);
     }
     return hip_status(hipGetLastError());
 }
@@ -1376,8 +1371,6 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    kmws_status st = launch_scan(WireSize{descs, flags}, n, wire_off, c, s);
-    if (st != KMWS_OK || n == 0) return st;
     return launch_copy<true>(src, dst, dst_cap, wire_off, descs, flags, n, c, s);
 }
 
@@ -1391,8 +1384,6 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    kmws_status st = launch_scan(PayloadSize{descs}, n, dst_off, c, s);
-    if (st != KMWS_OK || n == 0) return st;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
 

@@ -29,20 +29,30 @@
 
 namespace kmws {
 
-// Payload store of a tile word: non-temporal (streams past the L2) or temporal
-// (the line stays in L2 and is written back on eviction).  Which one streams
-// faster depends on the batch's layout: on an aligned arena temporal stores ran
-// +0.3-1.0 points, on a packed wire image they lost 1.6-7
-// (profiles/r02bz_unmask_store_policy_ab.txt), so the policy is part of the
-// schedule.  `nt` is block-uniform (the apply grid's store policy resolved
-// against the plan's layout flag): a scalar branch around each store, ONE code
-// path -- two instantiations of the tile body behind a branch took the
-// uncapped kernel from 80 to 86 VGPRs, 6 to 5 waves per SIMD, and 4 KiB
-// fragments from 82 to 79 % (profiles/r03e_configs.jsonl).
-__device__ __forceinline__ void store_word(const u32x4& val, u32x4* p, bool nt)
+// Payload store of a tile word: non-temporal (streams past the L2; the
+// default) or temporal (the line stays in L2 and is written back on eviction).
+// On plain allocations non-temporal stores ran ahead on every layout -- the
+// aligned arena 0.82 vs 0.76, the packed wire 0.82 vs 0.76, 4 KiB fragments
+// 0.81 vs 0.76, cfg3's Zipf wire 0.81 vs 0.75 of peak
+// (profiles/r03m_unmask_schedule_sweep_plain_nt_fixed.jsonl) -- so temporal
+// stores are only a candidate of the per-batch autotune (round 2 saw them
+// win by 0.3-1 point on one placed aligned arena, r02bz_unmask_store_policy_ab.txt).
+// The policy is a template parameter of the apply grid, chosen on the host.
+// The stores are buffer stores through a per-tile resource with the cache
+// policy as an immediate: written as `if (nt) __builtin_nontemporal_store(..)
+// else *p = ..`, the compiler had merged the two and dropped the hint.
+constexpr int kBufNT = 2;  // buffer cache policy: nt (gfx950; == global_store ... nt)
+constexpr int kBufferRsrcWord3 = 0x00020000;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(uint8_t* base, uint64_t lo, uint64_t hi)
 {
-    if (nt) __builtin_nontemporal_store(val, p);
-    else *p = val;
+    return __builtin_amdgcn_make_buffer_rsrc(base + lo, (short)0, (int)((hi - lo + 15) & ~15ull), kBufferRsrcWord3);
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_word(const u32x4& val, __amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(val, rs, (int)off, 0, NT ? kBufNT : 0);
 }
 
 // Each lane owns V consecutive-block words: word w = tid + kBlock * i.
@@ -55,33 +65,26 @@ struct UnmaskCfg {
 
 // Tile -> first frame map.  Frame f owns tile starts in [start_f, next_f)
 // where start_0 = 0, start_f = off_f, next_f = off_{f+1} (span for the last).
-// Validates sortedness / non-overlap / bounds on the fly, and records in the
-// workspace head whether any frame starts off a tile boundary (the layout the
-// automatic store policy of the apply grid reads).
+// Validates sortedness / non-overlap / bounds on the fly.
 __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __restrict__ d, uint32_t n,
                                                           uint64_t span, uint32_t tile_shift,
                                                           uint32_t* __restrict__ map,
                                                           WsHead* __restrict__ head)
 {
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t T = 1ull << tile_shift;
-    bool unaligned = false;
-    if (f < n) {
-        const kmws_desc df = d[f];
-        const uint64_t next = (f + 1 < n) ? d[f + 1].off : span;
-        unaligned = (df.off & (T - 1)) != 0;
-        if (df.off > span || df.off + (uint64_t)df.len > next) {
-            atomicOr(&head->status, kStatusBadDesc);
-        } else {
-            const uint64_t start = f == 0 ? 0 : df.off;
-            const uint64_t b0 = (start + T - 1) >> tile_shift;
-            const uint64_t b1 = (next + T - 1) >> tile_shift;
-            for (uint64_t b = b0; b < b1; ++b) map[b] = f;
-            if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
-        }
+    if (f >= n) return;
+    const kmws_desc df = d[f];
+    const uint64_t next = (f + 1 < n) ? d[f + 1].off : span;
+    if (df.off > span || df.off + (uint64_t)df.len > next) {
+        atomicOr(&head->status, kStatusBadDesc);
+        return;
     }
-    // one atomic per block at most (a packed wire sets it from every block)
-    if (__syncthreads_or(unaligned) && threadIdx.x == 0) atomicOr(&head->layout, kLayoutUnaligned);
+    const uint64_t start = f == 0 ? 0 : df.off;
+    const uint64_t T = 1ull << tile_shift;
+    const uint64_t b0 = (start + T - 1) >> tile_shift;
+    const uint64_t b1 = (next + T - 1) >> tile_shift;
+    for (uint64_t b = b0; b < b1; ++b) map[b] = f;
+    if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
 }
 
 // Issue every payload load of a tile.  Full tiles load unconditionally so the
@@ -101,15 +104,16 @@ __device__ __forceinline__ void load_tile(const uint8_t* __restrict__ base, uint
 }
 
 // Mask and store a loaded tile.  f = the tile-map frame, ok = plan status clean.
-template <int V, bool FULL, bool TWO = false>
+template <int V, bool FULL, bool TWO = false, bool NT = true>
 __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t tile_lo, uint64_t tile_hi,
                                             const kmws_desc* __restrict__ d, uint32_t n,
                                             const uint32_t* __restrict__ map, uint32_t tile, bool ok,
                                             const u32x4 (&v)[V], uint64_t* s_off, uint64_t* s_end, uint32_t* s_key,
-                                            const u32x4* pre = nullptr, bool nt = true)
+                                            const u32x4* pre = nullptr)
 {
     using Cfg = UnmaskCfg<V>;
     const int tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, tile_lo, tile_hi);
     // frames [f, flast] are the only ones that can overlap the tile: flast's
     // region holds the next tile's start (the map's last entry is a sentinel)
     uint32_t f = map[tile];
@@ -124,7 +128,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
-            if (ok) store_word(v[i] ^ r, reinterpret_cast<u32x4*>(base + a), nt);
+            if (ok) store_word<NT>(v[i] ^ r, rs, (uint32_t)(a - tile_lo));
         }
         return;
     }
@@ -172,7 +176,7 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         for (int i = 0; i < V; ++i) {
             const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
             if (ok && (m[i].x | m[i].y | m[i].z | m[i].w) != 0u)
-                store_word(v[i] ^ m[i], reinterpret_cast<u32x4*>(base + a), nt);
+                store_word<NT>(v[i] ^ m[i], rs, (uint32_t)(a - tile_lo));
         }
         return;
     }
@@ -239,18 +243,8 @@ __device__ __forceinline__ void finish_tile(uint8_t* __restrict__ base, uint64_t
         const uint64_t a = tile_lo + 16u * (uint64_t)(tid + kBlock * i);
         const u32x4 mm = m[i];
         if (ok && (FULL || a < tile_hi) && (mm.x | mm.y | mm.z | mm.w) != 0u)
-            store_word(v[i] ^ mm, reinterpret_cast<u32x4*>(base + a), nt);
+            store_word<NT>(v[i] ^ mm, rs, (uint32_t)(a - tile_lo));
     }
-}
-
-// Payload store policy of an apply grid (the schedule's store bits): automatic
-// = temporal when every frame of the batch starts on a tile boundary (the plan's
-// layout flag, read after the payload loads), non-temporal otherwise; or forced.
-enum StorePolicy : uint32_t { kStoreAuto = 0, kStoreNT = 1, kStoreTemporal = 2 };
-
-__device__ __forceinline__ bool nt_stores(const WsHead* head, uint32_t store)
-{
-    return store == kStoreNT || (store == kStoreAuto && (head->layout & kLayoutUnaligned) != 0);
 }
 
 // One block for the partial last tile of a span (the split grids take the full
@@ -280,14 +274,13 @@ __global__ void __launch_bounds__(kBlock) unmask_tail_kernel(uint8_t* __restrict
 // take the remaining tiles in order; k = 1 is the in-order grid).  With c > 0
 // the span is cut into runs of c tiles instead, dealt round-robin to the k
 // residues of b (blocks go round-robin over the 8 XCDs: k = 8 gives each XCD
-// its own runs).  `store`: StorePolicy.
-template <int V, bool TWO = false>
+// its own runs).  NT: the payload store policy.
+template <int V, bool TWO = false, bool NT = true>
 __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restrict__ base,
                                                               const kmws_desc* __restrict__ d, uint32_t n,
                                                               const uint32_t* __restrict__ map,
                                                               const WsHead* __restrict__ head, uint32_t nfull,
-                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w,
-                                                              uint32_t store)
+                                                              uint32_t k, uint32_t c, uint32_t b0, uint32_t w)
 {
     using Cfg = UnmaskCfg<V>;
     __shared__ uint64_t s_off[Cfg::kCap];
@@ -326,17 +319,16 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
         if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
         load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
-                                  s_key, &pre, nt_stores(head, store));
+        finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                      s_key, &pre);
         return;
     }
 #endif
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
-    // the head (status, layout) is read after the payload loads: its latency
-    // hides under theirs, and the store policy is a block-uniform branch
-    finish_tile<V, true, TWO>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key,
-                              nullptr, nt_stores(head, store));
+    // the status is read after the payload loads: its latency hides under theirs
+    finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+                                  s_key);
 }
 
 // Small host batches: the decoder's payloads of one socket read or one loop
@@ -537,15 +529,17 @@ static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n
 // of the span streams several windows: 82-86 % on some placements in physical
 // HBM, 76 % on others; runs of 16 tiles per XCD hold 78-79 % on every placement;
 // profiles/r01f_unmask_placement.txt, r02al_unmask_schedules_2bpc.txt) and how the
-// payload is stored (temporal stores gain 0.3-1 point on tile-aligned batches and
-// lose 1.6-7 on packed wire images, r02bz_unmask_store_policy_ab.txt).
+// payload is stored (non-temporal by default; see store_word).
 //
 // A schedule belongs to ONE batch: kmws_unmask_autotune / kmws_unmask_set_schedule
 // record it for (workspace, descs, n, span), and apply uses it only for that
-// batch; every other batch gets the default: split 4 (the best or within 0.4
-// points of it on plain allocations of the aligned arena, the packed wire and
-// 4 KiB fragments, profiles/r03f_unmask_schedule_sweep_plain.jsonl), automatic
-// store policy.  The reference's handleDataMask (WSHandler.cpp:303-310) is stateless;
+// batch; every other batch gets the default, by the mean region (the same test
+// as the occupancy cap): split 4 for regions of a tile or more -- the best on
+// plain allocations of the aligned arena (0.82), the packed wire (0.82) and
+// cfg3's Zipf wire (0.81) -- and grouped XCD runs below -- the best on 4 KiB
+// fragments (0.81 vs 0.78 for split 4)
+// (profiles/r03m_unmask_schedule_sweep_plain_nt_fixed.jsonl); non-temporal
+// stores.  The reference's handleDataMask (WSHandler.cpp:303-310) is stateless;
 // so is every batch that was not tuned.
 struct Split {
     uint32_t k, c, w;
@@ -553,7 +547,10 @@ struct Split {
 constexpr uint32_t kKindMask = 0xFFu;
 constexpr uint32_t kSchedTemporal = KMWS_SCHED_TEMPORAL_STORES;
 constexpr uint32_t kSchedNT = KMWS_SCHED_NT_STORES;
-constexpr uint32_t kDefaultSchedule = KMWS_SCHED_SPLIT4;
+static uint32_t default_schedule(uint64_t span, uint32_t n)
+{
+    return n && span / n >= ProdCfg::kTile ? KMWS_SCHED_SPLIT4 : KMWS_SCHED_GROUPED_RUNS;
+}
 
 static bool split_of(uint32_t kind, Split* sp)
 {
@@ -576,10 +573,7 @@ static bool valid_schedule(uint32_t code)
            (code & ~(kKindMask | kSchedTemporal | kSchedNT)) == 0;
 }
 
-static uint32_t store_policy(uint32_t code)
-{
-    return (code & kSchedTemporal) ? kStoreTemporal : ((code & kSchedNT) ? kStoreNT : kStoreAuto);
-}
+static bool temporal_stores(uint32_t code) { return (code & kSchedTemporal) != 0; }
 
 struct TunedBatch {
     const void* ws;
@@ -596,11 +590,11 @@ static int g_tuned_next = 0;
 
 static uint32_t batch_schedule(const void* ws, const kmws_desc* descs, uint32_t n, uint64_t span)
 {
-    if (g_tuned_count.load(std::memory_order_acquire) == 0) return kDefaultSchedule;
+    if (g_tuned_count.load(std::memory_order_acquire) == 0) return default_schedule(span, n);
     std::lock_guard<std::mutex> lk(g_tuned_mu);
     for (const TunedBatch& t : g_tuned)
         if (t.ws == ws && t.descs == descs && t.n == n && t.span == span) return t.code;
-    return kDefaultSchedule;
+    return default_schedule(span, n);
 }
 
 // Records (or, code < 0, forgets) the schedule of one batch.  One entry per
@@ -643,18 +637,25 @@ static kmws_status launch_apply(uint32_t code, uint8_t* base, uint64_t span, con
     const WsHead* head = static_cast<const WsHead*>(workspace);
     const uint32_t* map = reinterpret_cast<const uint32_t*>(head + 1);
     const uint64_t nfull = span / ProdCfg::kTile;
-    const uint32_t store = store_policy(code);
+    const bool temporal = temporal_stores(code);
     // a launch may hold at most 2^32 work-items: huge spans go in pieces of blocks
     constexpr uint64_t kMaxBlocks = (1ull << 32) / kBlock / 2;
     const unsigned lds_pad = unmask_lds_pad(span, n);
     for (uint64_t b0 = 0; b0 < nfull; b0 += kMaxBlocks) {
-        const uint64_t nb = nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks;
-        if (lds_pad)
-            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, true>), dim3((uint32_t)nb), dim3(kBlock), lds_pad, s,
-                               base, descs, n, map, head, (uint32_t)nfull, sp.k, sp.c, (uint32_t)b0, sp.w, store);
+        const dim3 grid((uint32_t)(nfull - b0 < kMaxBlocks ? nfull - b0 : kMaxBlocks));
+        const uint32_t nf = (uint32_t)nfull, bb = (uint32_t)b0;
+        if (lds_pad && !temporal)
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, true, true>), grid, dim3(kBlock), lds_pad, s, base, descs,
+                               n, map, head, nf, sp.k, sp.c, bb, sp.w);
+        else if (lds_pad)
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, true, false>), grid, dim3(kBlock), lds_pad, s, base,
+                               descs, n, map, head, nf, sp.k, sp.c, bb, sp.w);
+        else if (!temporal)
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, false, true>), grid, dim3(kBlock), 0, s, base, descs, n,
+                               map, head, nf, sp.k, sp.c, bb, sp.w);
         else
-            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, false>), dim3((uint32_t)nb), dim3(kBlock), 0, s, base,
-                               descs, n, map, head, (uint32_t)nfull, sp.k, sp.c, (uint32_t)b0, sp.w, store);
+            hipLaunchKernelGGL((unmask_split_kernel<kUnmaskV, false, false>), grid, dim3(kBlock), 0, s, base, descs,
+                               n, map, head, nf, sp.k, sp.c, bb, sp.w);
     }
     if (ntiles > nfull)  // the partial last tile
         hipLaunchKernelGGL(unmask_tail_kernel<kUnmaskV>, dim3(1), dim3(kBlock), 0, s, base, span, descs, n, map, head,
@@ -758,7 +759,7 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
         return KMWS_ERR_FAILED;
     }
     float best = 1e30f;
-    uint32_t pick = kDefaultSchedule;
+    uint32_t pick = default_schedule(span, n);
     for (int rep = 0; rep < 2 && st == KMWS_OK; ++rep) {
         for (uint32_t kind : kinds) {
             for (uint32_t store : {kSchedNT, kSchedTemporal}) {

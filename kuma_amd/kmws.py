@@ -52,7 +52,11 @@ BENCH_EXPORTS = [
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
 SCHED_GROUPED_RUNS, SCHED_IN_ORDER, SCHED_SPLIT2, SCHED_SPLIT8, SCHED_XCD_RUNS, SCHED_SPLIT4 = 0, 1, 2, 3, 4, 5
 SCHED_KINDS = (0, 1, 2, 3, 4, 5)
-SCHED_DEFAULT = SCHED_SPLIT4  # what kmws_unmask_apply uses for a batch nobody tuned
+
+
+def sched_default(span: int, n: int) -> int:
+    """The schedule kmws_unmask_apply uses for a batch nobody tuned."""
+    return SCHED_SPLIT4 if n and span // n >= 16384 else SCHED_GROUPED_RUNS
 SCHED_NT_STORES, SCHED_TEMPORAL_STORES = 1 << 29, 1 << 30
 
 
@@ -70,7 +74,9 @@ _lib: Optional[C.CDLL] = None
 
 
 def lib_path() -> str:
-    return _build.LIB
+    # KMWS_LIB: an A/B tuning build of the same ABI (tools only; the product
+    # library is kuma_amd/lib/libkmws_gpu.so)
+    return os.environ.get("KMWS_LIB") or _build.LIB
 
 
 def lib() -> C.CDLL:
@@ -86,8 +92,8 @@ def lib() -> C.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    path = _build.LIB
-    if not _build.up_to_date():
+    path = lib_path()
+    if path == _build.LIB and not _build.up_to_date():
         try:
             _build.build()
         except (OSError, Exception) as e:  # no hipcc on this machine: use the shipped .so

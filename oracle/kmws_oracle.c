@@ -10,13 +10,17 @@
  * reference checkout).  No reference source is copied: the byte semantics are
  * restated in plain C, including the reference's quirks.
  *
- * Pinning: the reference's WSHandler.cpp cannot be compiled in this image
- * without writing stand-ins for the absent libkev headers (third_party/libkev
- * is an empty submodule), which this build does not do.  The restatement is
- * therefore pinned by (1) the reference outputs recorded in SURVEY.md sec.8
- * (a-2, a-4, a-5 tables, produced by running the reference WSHandler.cpp in
- * the survey container) and (2) the RFC 6455 sec.5.7 known-answer frames; both
- * live in tests/golden/reference_vectors.json.  See DESIGN.md "Oracle".
+ * PARITY UNPINNED.  The reference's WSHandler.cpp cannot be compiled in this
+ * image without writing stand-ins for the absent libkev headers
+ * (third_party/libkev is an empty submodule), which this build does not do,
+ * and the reference's own tests hold no WebSocket vectors (unittest/ covers
+ * KMBuffer and Base64 only).  So no reference-held or reference-run fixture
+ * checks this restatement.  What checks it (tests/golden/reference_vectors.json):
+ * the RFC 6455 sec.5.7 known-answer frames -- independent of kuma, they pin the
+ * protocol-defined parts (masking, the three length classes, fragmentation) --
+ * and values transcribed from SURVEY.md sec.8 (a-2, a-4, a-5 tables, from a
+ * survey-session build of WSHandler.cpp that needed stand-in headers: a record,
+ * not a pin).  See DESIGN.md sec.2 "Oracle".
  */
 #include <stdint.h>
 #include <stdlib.h>

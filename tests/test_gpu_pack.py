@@ -343,16 +343,3 @@ def test_find_headers_streams_matches_host_walk(T):
             i += 1
     assert i == len(hl)
     assert ends  # some complete streams were checked
-
-
-@pytest.mark.parametrize("chunks", [3, 8])
-def test_pack_chunks_knob(T, chunks):
-    """The chunked pack pipeline (KMWS_PACK_CHUNKS, read once per process) in a
-    child process: encode and gather-unmask bit-exact vs the oracle."""
-    import subprocess
-    import sys
-    env = dict(os.environ, KMWS_PACK_CHUNKS=str(chunks))
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "pack_chunks_child.py")], env=env,
-                       capture_output=True, text=True, timeout=150)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert f"pack chunks ok {chunks}" in r.stdout

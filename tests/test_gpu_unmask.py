@@ -229,8 +229,9 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     assert _valid_schedule(choice) and choice & (3 << 29)  # the autotune times forced store policies
     assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == choice
     ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
-    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_DEFAULT  # other batches: default
-    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.SCHED_DEFAULT  # other span
+    dflt = kmws.sched_default(len(buf), len(descs))
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == dflt  # other batches: default
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.sched_default(len(buf) - 16, len(descs))
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
@@ -238,15 +239,14 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     torch.cuda.synchronize()
     assert ws.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
     kmws.unmask_set_schedule(ws, d_desc, len(buf), -1)  # forget: back to the default
-    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == kmws.SCHED_DEFAULT
+    assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == dflt
 
 
 def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
     """ADVICE r02 / VERDICT r02 #4: tuning an aligned arena (which may pick
     temporal stores) must not change how a packed wire image is unmasked later
-    in the same process: the wire keeps the default schedule, and the plan's
-    layout flag (workspace word 1) makes its automatic store policy
-    non-temporal; the aligned batch's flag selects temporal stores."""
+    in the same process: the wire keeps the default schedule (non-temporal
+    stores), and both batches stay bit-exact."""
     torch = torch_dev
     from kuma_amd import kmws
     n, L = 4096, 65536
@@ -256,20 +256,20 @@ def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
     kmws.fill_synthetic(base, 5)
     kmws.fill_uniform_descs(descs, L, L, 6)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
-    kmws.unmask_autotune(base, descs, ws, span)
-    kmws.unmask_plan(descs, ws, span)
-    torch.cuda.synchronize()
-    assert int(ws.tensor[4:8].cpu().view(torch.int32)[0]) == 0  # every frame on a tile boundary
+    kmws.unmask_set_schedule(ws, descs, span, kmws.SCHED_SPLIT2 | kmws.SCHED_TEMPORAL_STORES)  # as a tune may pick
+    assert kmws.unmask_get_schedule(ws, descs, span) == kmws.SCHED_SPLIT2 | kmws.SCHED_TEMPORAL_STORES
+    picked = kmws.unmask_autotune(base, descs, ws, span)
+    assert kmws.unmask_get_schedule(ws, descs, span) == picked
     rng = np.random.default_rng(77)
     buf, wd = layout("packed_wire", rng)
     d_buf, d_desc = _to_dev(torch, buf, wd)
     ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
-    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == kmws.SCHED_DEFAULT
+    got = kmws.unmask_get_schedule(ws2, d_desc, len(buf))
+    assert got == kmws.sched_default(len(buf), len(wd)) and not got & kmws.SCHED_TEMPORAL_STORES
     want = buf.copy()
     orc.unmask_batch(want, wd)
     kmws.unmask_batch(d_buf, d_desc, ws2, len(buf))
     torch.cuda.synchronize()
-    assert int(ws2.tensor[4:8].cpu().view(torch.int32)[0]) == 1  # unaligned: automatic stores are non-temporal
     assert ws2.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
     kmws.unmask_batch(base, descs, ws, span)  # the aligned batch under its tuned schedule
     assert ws.status() == 0 and kmws.check_unmasked(base, 5, descs) == 0
