@@ -12,14 +12,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
 
-// First 16 bytes of every workspace: status word (+ the scan's ticket
-// counter), zeroed by a kernel (not a memset node: see launch_zero) at the
+// First 16 bytes of every workspace: status word, zeroed by a kernel (not a memset node: see launch_zero) at the
 // start of each batch call.
 struct WsHead {
     uint32_t status;
-    uint32_t pad0;
-    uint32_t ticket;  // tile tickets of the single-pass scans (kmws_pack.hip)
-    uint32_t pad1;
+    uint32_t pad[3];
 };
 constexpr uint32_t kStatusBadDesc = 1u;
 constexpr uint32_t kStatusBadHeader = 2u;

@@ -4,12 +4,14 @@
 // (src/ws/WSHandler.cpp:46-106) followed by the masked payload
 // (WebSocket::Impl::sendWsFrame, src/ws/WebSocketImpl.cpp:381-404): the wire
 // image is header_0 payload_0 header_1 payload_1 ...  Kernels:
-//   1. scan_kernel: one single-pass (decoupled look-back) exclusive scan of two
-//      per-frame values -- the wire size (2/4/10 + 4*mask + len) -> wire_off,
-//      and an upper bound on the frame's wave units -> unit slot bases;
-//   2. prologue_kernel, 256 frames per block: the few words around each
-//      frame's boundaries (header bytes, the next frame's first bytes),
-//      composed byte-exactly, and one 32-byte record per wave unit;
+//   1. reduce_kernel, 2048 frames per block: two per-frame values -- the wire
+//      size (2/4/10 + 4*mask + len) and an upper bound on the frame's wave
+//      units -- summed per 256-frame row and per tile; scan_tiles_kernel
+//      (one block) scans the tile totals;
+//   2. prologue_kernel, 256 frames per block: each frame's wire offset and
+//      first unit slot (row prefix + block scan), the few words around its
+//      boundaries (header bytes, the next frame's first bytes), composed
+//      byte-exactly, and one 32-byte record per wave unit;
 //   3. copy_kernel: one wave per unit of a frame's owned 64-byte granules;
 //      interior words are loaded, funnel-shifted and XORed with the rotated
 //      key, edge words are merged in; every granule is written once, by one
@@ -19,15 +21,15 @@
 // (WSHandler.cpp:118-234, including the 127-length quirk); the payload is then
 // unmasked in place (kmws_unmask_batch) or gathered + unmasked into a dense
 // arena by the same copy kernels (kmws_gather_unmask).
-// Header-only pack (kmws_pack_headers, kuma's iovec form): the scan's emit
-// pass writes each header into a 16-byte slot.  Boundary discovery on the
+// Header-only pack (kmws_pack_headers, kuma's iovec form): each header into a
+// 16-byte slot, with the wire offsets after reduce_kernel.  Boundary discovery on the
 // device (kmws_find_headers_streams): the serial header-chain walk, one lane
 // per stream.
 #include "kmws_common.hpp"
 
 namespace kmws {
 
-constexpr int kScanItems = 8;                      // frames per lane in the scan
+constexpr int kScanItems = 8;                      // frames per lane in reduce_kernel
 constexpr int kScanTile = kBlock * kScanItems;     // 2048 frames per block
 
 __host__ __device__ __forceinline__ uint32_t hdr_len(uint32_t len, uint32_t mask)
@@ -110,25 +112,27 @@ __host__ __device__ __forceinline__ uint64_t unit_bound(uint64_t R)
            kUnitWords;
 }
 
+// Per-frame quantities: load() reads what they depend on, value() computes
+// them (split so a caller can issue many frames' loads before one wait).
+struct SizeRaw {
+    uint32_t len, fl;
+};
 struct WireSize {
     static constexpr bool kHeaders = true;
     const kmws_desc* d;
     const uint16_t* flags;
-    __device__ V2 operator()(uint32_t f) const
+    __device__ SizeRaw load(uint32_t f) const { return SizeRaw{d[f].len, flags[f]}; }
+    __device__ V2 value(SizeRaw x) const
     {
-        const uint32_t len = d[f].len;
-        const uint64_t r = (uint64_t)hdr_len(len, (flags[f] >> 8) & 1u) + len;
+        const uint64_t r = (uint64_t)hdr_len(x.len, (x.fl >> 8) & 1u) + x.len;
         return V2{r, unit_bound(r)};
     }
 };
 struct PayloadSize {
     static constexpr bool kHeaders = false;
     const kmws_desc* d;
-    __device__ V2 operator()(uint32_t f) const
-    {
-        const uint64_t r = d[f].len;
-        return V2{r, unit_bound(r)};
-    }
+    __device__ SizeRaw load(uint32_t f) const { return SizeRaw{d[f].len, 0u}; }
+    __device__ V2 value(SizeRaw x) const { return V2{x.len, unit_bound(x.len)}; }
 };
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x)
@@ -149,198 +153,119 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x)
     return x;
 }
 
-// Single-pass scan (decoupled look-back).  A block scans 2048 frames, read
-// row-striped (frame base + i*kBlock + tid) so every load is coalesced.  Blocks
-// take their tile in ticket order (an atomic counter in the workspace head),
-// publish their tile's aggregate at once and its inclusive prefix as soon as
-// their look-back resolved: a block only ever waits on blocks that started
-// before it, so the grid always makes progress, and one launch replaces the
-// reduce / scan-partials / emit launches (and the second read of the
-// descriptors) of a three-pass scan.  Tile state: per quantity one 64-bit word,
-// (flag << 62) | value, written and read with device-scope atomics (the L2s of
-// the 8 XCDs are not coherent for plain accesses); a state is taken when both
-// words carry the same flag.
-struct ScanState {
-    uint64_t a, b;
-};
-constexpr uint64_t kFlagAgg = 1ull, kFlagInc = 2ull, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 22;  // ~0.1-1 s: a lost predecessor sets the status instead of hanging
+// Two-level scan.  reduce_kernel: a block sums 2048 frames (8 rows of 256,
+// read row-striped so every load is coalesced) and writes each row's exclusive
+// prefix inside the tile to grp[] and the tile's total to tiles[];
+// scan_tiles_kernel (one block) turns tiles[] into exclusive prefixes and
+// writes the grand totals.  The per-frame offsets are emitted by the kernel
+// that reads each 256-frame row next (the prologue, or the header-slot kernel):
+// two loads give the row's prefix, a block scan the frame's.  Measured on 4 M
+// frames: a decoupled look-back scan (one launch, tiles publishing aggregates
+// and inclusive prefixes through device-scope atomics) 95-115 us; the reduce
+// with the last block scanning the totals (a device-scope fence per block
+// before its counter increment, i.e. an L2 write-back) 65-94 us.
+constexpr int kRowsPerTile = kScanItems;  // 256-frame rows per 2048-frame tile
 
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
+// Exclusive scan over the block (256 threads); `total` = the block's sum.
+// s_w: 4 entries of LDS, free on entry (the caller syncs before reusing them).
+__device__ __forceinline__ V2 block_excl_scan(V2 v, V2* __restrict__ s_w, V2& total)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void publish(ScanState* st, uint64_t flag, V2 v)
-{
-    st_agent(&st->a, flag << 62 | (v.a & kValMask));
-    st_agent(&st->b, flag << 62 | (v.b & kValMask));
-}
-
-// Wave 0 of tile `tile`: the exclusive prefix of the tiles before it.  The
-// wave looks at a window of 256 tiles below j = tile - 1 at once (lane l, item
-// k: tile j - l - 64 k; four independent loads per lane); the window's tiles up
-// to and including the nearest one with an inclusive prefix contribute
-// (nonexistent tiles below 0 count as an inclusive zero); without one the
-// window's aggregates are summed and the window moves 256 tiles back.  With
-// every tile of a grid starting at once, the prefixes propagate through chains
-// of aggregates, so a window of 64 made tile 1,000 wait for ~16 dependent
-// rounds of loads; 256 makes it 4.
-constexpr int kLookItems = 4;
-__device__ V2 look_back(const ScanState* __restrict__ st, uint32_t tile, WsHead* __restrict__ head)
-{
-    const int lane = threadIdx.x & 63;
-    V2 ex{0, 0};
-    for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64 * kLookItems) {
-        uint32_t flag[kLookItems];  // 0: not published yet, kFlagAgg, kFlagInc (tiles below 0: an inclusive zero)
-        uint64_t va[kLookItems], vb[kLookItems];
-#pragma unroll
-        for (int k = 0; k < kLookItems; ++k) {
-            flag[k] = j - lane - 64 * k < 0 ? (uint32_t)kFlagInc : 0u;
-            va[k] = vb[k] = 0;
-        }
-        for (uint32_t spins = 0;; ++spins) {
-            bool done = true;
-#pragma unroll
-            for (int k = 0; k < kLookItems; ++k) {
-                if (flag[k] != 0) continue;
-                const int64_t p = j - lane - 64 * k;
-                const uint64_t A = ld_agent(&st[p].a), B = ld_agent(&st[p].b);
-                if ((A >> 62) != 0 && (A >> 62) == (B >> 62)) {
-                    flag[k] = (uint32_t)(A >> 62);
-                    va[k] = A & kValMask;
-                    vb[k] = B & kValMask;
-                } else {
-                    done = false;
-                }
-            }
-            if (__all(done)) break;
-            if (spins >= kSpinLimit) {  // cannot happen: every ticketed tile publishes
-                atomicOr(&head->status, kStatusBadDesc);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        // the nearest inclusive tile in distance order (item k, then lane)
-        int first_k = kLookItems, first_l = 64;
-#pragma unroll
-        for (int k = kLookItems - 1; k >= 0; --k) {
-            const uint64_t inc = __ballot(flag[k] == (uint32_t)kFlagInc);
-            if (inc) {
-                first_k = k;
-                first_l = __ffsll((unsigned long long)inc) - 1;
-            }
-        }
-        V2 part{0, 0};
-#pragma unroll
-        for (int k = 0; k < kLookItems; ++k) {
-            const bool take = k < first_k || (k == first_k && lane <= first_l);
-            part.a += take ? va[k] : 0;
-            part.b += take ? vb[k] : 0;
-        }
-        ex.a += wave_sum(part.a);
-        ex.b += wave_sum(part.b);
-        if (first_k < kLookItems) break;
-    }
-    return ex;
-}
-
-// Region offsets -> out_a (n+1 entries, out_a[n] = total), unit slot bases ->
-// out_b.  (hdr != nullptr: also frame f's header bytes into the 16-byte slot
-// hdr[f] and its length into hl_out[f] -- kmws_pack_headers; Size is WireSize.)
-template <class Size>
-__global__ void __launch_bounds__(kBlock) scan_kernel(Size size, uint32_t n, uint32_t ntiles,
-                                                      ScanState* __restrict__ st, WsHead* __restrict__ head,
-                                                      uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_b,
-                                                      u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
-{
-    __shared__ V2 s_row[kScanItems][kBlock / 64];
-    __shared__ V2 s_prefix;
-    __shared__ uint32_t s_tile;
-    if (threadIdx.x == 0) s_tile = atomicAdd(&head->ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t base = (uint64_t)tile * kScanTile + threadIdx.x;
-    // 1. row totals per wave (values not kept: the emit pass re-reads the frames,
-    //    cache-hot, so no per-frame state lives in registers across the look-back)
-    V2 v[kScanItems];
+    const V2 inc{wave_incl_scan(v.a), wave_incl_scan(v.b)};
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    V2 before{0, 0};
+    total = V2{0, 0};
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        const uint64_t f = base + (uint64_t)i * kBlock;
-        v[i] = f < n ? size((uint32_t)f) : V2{0, 0};
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const V2 t = s_w[w];
+        if (w < wave) before = before + t;
+        total = total + t;
+    }
+    return V2{before.a + inc.a - v.a, before.b + inc.b - v.b};
+}
+
+// Loads are coalesced (row-striped: frame i * 256 + thread, all 16 issued
+// before one wait) and staged in LDS; each thread then sums 8 consecutive
+// frames, and a row's total is one 32-lane reduction (a wave-wide 64-bit
+// reduction per row and quantity -- 16 per thread -- made the kernel ALU-bound:
+// 24-36 us on 4 M frames).
+constexpr uint32_t kPastEnd = 1u << 31;  // SizeRaw.fl: a slot past the batch
+template <class Size>
+__global__ void __launch_bounds__(kBlock) reduce_kernel(Size size, uint32_t n, V2* __restrict__ tiles,
+                                                        V2* __restrict__ grp)
+{
+    __shared__ SizeRaw s_raw[kScanTile];
+    __shared__ V2 s_row[kRowsPerTile];
+    const uint32_t t = threadIdx.x;
+    const uint64_t F = (uint64_t)blockIdx.x * kScanTile;
+    SizeRaw raw[kRowsPerTile];
+#pragma unroll
+    for (int i = 0; i < kRowsPerTile; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        raw[i] = size.load((uint32_t)__builtin_elementwise_min(f, (uint64_t)n - 1));
     }
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        const V2 t{wave_sum(v[i].a), wave_sum(v[i].b)};
-        if (lane == 0) s_row[i][wave] = t;
+    for (int i = 0; i < kRowsPerTile; ++i) {
+        if (F + (uint64_t)i * kBlock + t >= n) raw[i].fl |= kPastEnd;
+        s_raw[i * kBlock + t] = raw[i];
     }
     __syncthreads();
-    // 2. the tile's aggregate, published; its prefix by look-back (wave 0)
-    if (wave == 0) {
-        V2 agg{0, 0};
+    V2 sum{0, 0};  // frames 8t .. 8t + 7 of the tile: row t / 32
 #pragma unroll
-        for (int i = 0; i < kScanItems; ++i)
+    for (int k = 0; k < kScanItems; ++k) {
+        const SizeRaw r = s_raw[kScanItems * t + k];
+        if (!(r.fl & kPastEnd)) sum = sum + size.value(r);
+    }
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) agg = agg + s_row[i][w];
+    for (int o = 16; o > 0; o >>= 1) {
+        sum.a += __shfl_xor(sum.a, o, 64);
+        sum.b += __shfl_xor(sum.b, o, 64);
+    }
+    if ((t & 31u) == 0) s_row[t >> 5] = sum;
+    __syncthreads();
+    if (t <= (unsigned)kRowsPerTile) {  // thread i < 8: row i's prefix; thread 8: the tile's total
         V2 pre{0, 0};
-        if (tile == 0) {
-            if (lane == 0) publish(&st[0], kFlagInc, agg);
-        } else {
-            if (lane == 0) publish(&st[tile], kFlagAgg, agg);
-            pre = look_back(st, tile, head);
-            if (lane == 0) publish(&st[tile], kFlagInc, pre + agg);
-        }
-        if (lane == 0) {
-            s_prefix = pre;
-            if (tile == ntiles - 1) {  // the grand totals
-                out_a[n] = pre.a + agg.a;
-                if (out_b) out_b[n] = pre.b + agg.b;
-            }
-        }
-    }
-    __syncthreads();
-    // 3. emit: frame (i, wave, lane) follows rows < i (all waves) and waves < wave of row i
-    V2 run = s_prefix;
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        V2 before{0, 0}, row{0, 0};
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const V2 t = s_row[i][w];
-            if (w < wave) before = before + t;
-            row = row + t;
-        }
-        const uint64_t f = base + (uint64_t)i * kBlock;
-        const V2 x = f < n ? size((uint32_t)f) : V2{0, 0};
-        const V2 inc{wave_incl_scan(x.a), wave_incl_scan(x.b)};
-        if (f < n) {
-            out_a[f] = run.a + before.a + inc.a - x.a;
-            if (out_b) out_b[f] = run.b + before.b + inc.b - x.b;
-            if constexpr (Size::kHeaders) {
-                if (hdr) {
-                    const kmws_desc dx = size.d[f];
-                    const uint32_t fl = size.flags[f];
-                    uint64_t h0, h1;
-                    build_header(dx.len, fl, dx.key, h0, h1);
-                    hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                    if (hl_out) hl_out[f] = (uint8_t)hdr_len(dx.len, (fl >> 8) & 1u);
-                }
-            }
-        }
-        run = run + row;
+        for (uint32_t r = 0; r < (uint32_t)kRowsPerTile; ++r)
+            if (r < t) pre = pre + s_row[r];
+        const uint64_t g = (uint64_t)blockIdx.x * kRowsPerTile + t;
+        if (t == (unsigned)kRowsPerTile) tiles[blockIdx.x] = pre;
+        else if (g * kBlock < n) grp[g] = pre;
     }
 }
 
-// Zeroes the workspace head and the scan's tile states (one launch; a memset
-// node replayed in a captured graph was seen writing garbage, kmws_common.hpp).
-__global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict__ p, uint64_t words)
+// tiles[0, ntiles) -> exclusive prefixes, tiles[ntiles] = the totals (also
+// out_a[n]: the caller's offsets array has n + 1 entries).  One block.
+__global__ void __launch_bounds__(kBlock) scan_tiles_kernel(V2* __restrict__ tiles, uint32_t ntiles,
+                                                            uint64_t* __restrict__ out_a, uint32_t n)
 {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
-        p[i] = 0;
+    __shared__ V2 s_w[kBlock / 64];
+    constexpr int K = 8;
+    V2 carry{0, 0};
+    for (uint64_t c = 0; c < ntiles; c += (uint64_t)kBlock * K) {
+        V2 t[K], sum{0, 0};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t j = c + (uint64_t)threadIdx.x * K + k;
+            t[k] = j < ntiles ? tiles[j] : V2{0, 0};
+            sum = sum + t[k];
+        }
+        V2 tot;
+        V2 run = carry + block_excl_scan(sum, s_w, tot);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t j = c + (uint64_t)threadIdx.x * K + k;
+            if (j < ntiles) tiles[j] = run;
+            run = run + t[k];
+        }
+        carry = carry + tot;
+        __syncthreads();  // s_w is reused
+    }
+    if (threadIdx.x == 0) {
+        tiles[ntiles] = carry;
+        out_a[n] = carry.a;
+    }
 }
 
 // Dword I of the 8-dword window lo||hi (I fixed at compile time).
@@ -421,27 +346,6 @@ struct FrameGeom {
     uint32_t key;         // key to apply (0 = none)
     uint32_t len;
 };
-
-template <bool HEADERS>
-__device__ __forceinline__ FrameGeom geom(uint32_t f, const uint64_t* __restrict__ start,
-                                          const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags)
-{
-    const kmws_desc x = d[f];
-    FrameGeom g;
-    g.r0 = start[f];
-    uint32_t hl = 0;
-    g.key = x.key;
-    if (HEADERS) {
-        const uint32_t mask = (flags[f] >> 8) & 1u;
-        hl = hdr_len(x.len, mask);
-        if (!mask) g.key = 0;
-    }
-    g.p0 = g.r0 + hl;
-    g.r1 = g.p0 + x.len;
-    g.sdel = x.off - g.p0;
-    g.len = x.len;
-    return g;
-}
 
 // Output words of a frame: owned [olo, ohi), interior [ilo, ihi) inside them,
 // and its units (bases b0, b0 + 256, ...).
@@ -594,13 +498,9 @@ struct FrameUnits {
     uint32_t rk, units, head_f, nedge;
 };
 
-// Scan + everything the copy waves need of 256 frames, one block (one launch
-// for the whole batch, blocks in ticket order):
-//   the scan: the block's region sizes (header + payload) and unit-slot bounds
-//     scanned in LDS, the block's exclusive prefix by decoupled look-back
-//     (look_back), frame offsets -> start[f] and unit slot bases -> ubase[f]
-//     (start[n], ubase[n] = the totals, by the last block); frame f+1's region
-//     starts where frame f's ends, so a block needs no other block's offsets;
+// Everything the copy waves need of 256 frames, one block (after
+// reduce_kernel: the row's prefix and a block scan give each frame's region
+// offset, written to start[], and its first unit slot):
 //   edge words -- a frame's owned words outside its interior: q < head_f at
 //     olo + q, then the tail at ihi + (q - head_f) -- one thread per frame,
 //     into LDS, then written out over one contiguous run edge[F0 * kEdgeWords ...]
@@ -617,81 +517,47 @@ struct FrameUnits {
 // of frame f+1 from which every tail word funnels its payload bytes (window
 // indices clamped to f+1's payload; clamped words only feed bytes outside it,
 // which are masked off).  The rare word a third region reaches into (a frame
-// ending inside it) is composed byte by byte.  Owned words past the end of the
-// output (the last frame's last granule) are composed as zero and never stored
-// by the copy waves, which clip at the total.  Capacity: a block whose regions
-// end past `cap` sets the status and writes no record or edge word (its slots
-// could lie past the workspace); the copy waves then write nothing.
+// ending inside it) is composed byte by byte.  Frame f+1's region starts where
+// frame f's ends, so only frame f's offset is read.  Owned words past the end
+// of the output (the last frame's last granule) are composed as zero and never
+// stored by the copy waves, which clip at the total.  Also the capacity check
+// (status set if the output exceeds cap; nothing is written then).
+//
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) scan_prologue_kernel(const uint8_t* __restrict__ src,
-                                                               const kmws_desc* __restrict__ d,
-                                                               const uint16_t* __restrict__ flags, uint32_t n,
-                                                               uint32_t ntiles, uint64_t cap,
-                                                               ScanState* __restrict__ st, WsHead* __restrict__ head,
-                                                               uint64_t* __restrict__ start,
-                                                               uint64_t* __restrict__ ubase, UnitRec* __restrict__ rec,
-                                                               u32x4* __restrict__ edge)
+__global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          uint64_t cap, WsHead* __restrict__ head,
+                                                          const V2* __restrict__ tiles, uint32_t ntiles,
+                                                          const V2* __restrict__ grp, uint64_t* __restrict__ start,
+                                                          UnitRec* __restrict__ rec, u32x4* __restrict__ edge)
 {
     __shared__ FrameUnits s_fu[kBlock];
     __shared__ uint32_t s_ub[kBlock + 1];
     __shared__ u32x4 s_edge[kBlock * kEdgeWords];
     __shared__ uint8_t s_ne[kBlock];  // live edge words per frame
-    __shared__ V2 s_wave[kBlock / 64];
-    __shared__ V2 s_pre;
-    __shared__ uint32_t s_tile;
+    __shared__ V2 s_w[kBlock / 64];
     const uint32_t t = threadIdx.x;
-    const int lane = t & 63, wave = t >> 6;
-    if (t == 0) s_tile = atomicAdd(&head->ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint64_t F0 = (uint64_t)tile * kBlock;
+    const uint64_t F0 = (uint64_t)blockIdx.x * kBlock;
     const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
     const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
+    // totals, the row's prefix and the three frames' descriptors: one latency level
+    const V2 tot = tiles[ntiles];
+    const V2 pre = tiles[blockIdx.x / kRowsPerTile] + grp[blockIdx.x];
+    const uint64_t total = tot.a;
     kmws_desc x[kPre];
     uint32_t fl[kPre];
     load_descs<HEADERS>(f, n, x, fl, d, flags);
-    // this frame's region and unit-slot bound, scanned over the block
-    const uint32_t hl0 = HEADERS ? hdr_len(x[0].len, (fl[0] >> 8) & 1u) : 0u;
-    const uint64_t R = t < nf ? (uint64_t)hl0 + x[0].len : 0, U = unit_bound(R);
-    const uint64_t incR = wave_incl_scan(R), incU = wave_incl_scan(U);
-    if (lane == 63) s_wave[wave] = V2{incR, incU};
-    __syncthreads();
-    V2 before{0, 0}, agg{0, 0};
-#pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
-        const V2 v = s_wave[w];
-        if (w < wave) before = before + v;
-        agg = agg + v;
-    }
-    if (wave == 0) {
-        V2 pre{0, 0};
-        if (tile == 0) {
-            if (lane == 0) publish(&st[0], kFlagInc, agg);
-        } else {
-            if (lane == 0) publish(&st[tile], kFlagAgg, agg);
-            pre = look_back(st, tile, head);
-            if (lane == 0) publish(&st[tile], kFlagInc, pre + agg);
-        }
-        if (lane == 0) {
-            s_pre = pre;
-            if (tile == ntiles - 1) {  // the grand totals
-                start[n] = pre.a + agg.a;
-                ubase[n] = pre.b + agg.b;
-            }
-        }
-    }
-    __syncthreads();
-    const V2 pre = s_pre;
-    const uint64_t r0 = pre.a + before.a + incR - R, uf = pre.b + before.b + incU - U;
-    if (t < nf) {
-        start[f] = r0;
-        ubase[f] = uf;
-    }
-    if (pre.a + agg.a > cap) {  // block-uniform: records would not fit the workspace; the copy waves see the status
-        if (t == 0) atomicOr(&head->status, kStatusBadDesc);
+    // this frame's region offset and first unit slot
+    V2 row;
+    const uint64_t rsz = (uint64_t)(HEADERS ? hdr_len(x[0].len, (fl[0] >> 8) & 1u) : 0u) + x[0].len;
+    const V2 off = pre + block_excl_scan(t < nf ? V2{rsz, unit_bound(rsz)} : V2{0, 0}, s_w, row);
+    const uint64_t r0 = off.a, uf = off.b, S0 = pre.b, uend = pre.b + row.b;
+    if (t < nf) start[f] = r0;
+    if (total > cap) {  // records would not fit the workspace; the copy waves see the status (block-uniform)
+        if (F0 == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
         return;
     }
-    const uint64_t S0 = pre.b, uend = pre.b + agg.b;
     FrameGeom g[kPre];
     g[0] = geom_at<HEADERS>(x[0], fl[0], r0);
 #pragma unroll
@@ -977,10 +843,7 @@ __device__ __forceinline__ void unit_finish(const UnitInfo& x, int lane, uint8_t
 // One wave per unit: kUnitW words per lane, 1 KiB per wave-instruction.
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                      const uint64_t* __restrict__ start,
-                                                      const kmws_desc* __restrict__ d,
-                                                      const uint16_t* __restrict__ flags, uint32_t n,
-                                                      const uint64_t* __restrict__ ubase,
+                                                      const V2* __restrict__ tot,
                                                       const UnitRec* __restrict__ rec,
                                                       const u32x4* __restrict__ edge,
                                                       const WsHead* __restrict__ head, uint64_t unit_base,
@@ -1004,9 +867,9 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     // record, slot count, status and total are independent scalar loads (one
     // latency level); slots past the count lie inside the workspace and are ignored
     const UnitRec r = rec[u];
-    const uint64_t total_units = ubase[n];
+    const uint64_t total_units = tot->b;
     const uint32_t st = head->status;
-    const uint64_t total = start[n];
+    const uint64_t total = tot->a;
     // no early exit between these loads and their uses (the compiler would sink
     // the record load below the count's wait): an out-of-range wave owns no words
     const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
@@ -1145,19 +1008,34 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
 
 // ------------------------------ header pack only ------------------------------
 // One lane per frame: the header bytes of WSHandler::encodeFrameHeader in a
-// 16-byte slot (one coalesced store per lane) and its length.
+// 16-byte slot (one coalesced store per lane) and its length; with OFFSETS
+// (after reduce_kernel) also the frame's wire offset, the row's prefix plus a
+// block scan.
+template <bool OFFSETS>
 __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* __restrict__ d,
                                                               const uint16_t* __restrict__ flags, uint32_t n,
-                                                              u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
+                                                              u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out,
+                                                              const V2* __restrict__ tiles,
+                                                              const V2* __restrict__ grp, uint64_t* __restrict__ out)
 {
+    __shared__ V2 s_w[kBlock / 64];
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    if (f >= n) return;
-    const kmws_desc x = d[f];
-    const uint32_t fl = flags[f];
+    const bool live = f < n;
+    const kmws_desc x = d[live ? f : n - 1];
+    const uint32_t fl = flags[live ? f : n - 1];
+    const uint32_t hl = hdr_len(x.len, (fl >> 8) & 1u);
+    if (OFFSETS) {
+        const V2 pre = tiles[blockIdx.x / kRowsPerTile] + grp[blockIdx.x];
+        V2 row;
+        const uint64_t r = (uint64_t)hl + x.len;
+        const V2 off = pre + block_excl_scan(live ? V2{r, 0} : V2{0, 0}, s_w, row);
+        if (live) out[f] = off.a;
+    }
+    if (!live) return;
     uint64_t h0, h1;
     build_header(x.len, fl, x.key, h0, h1);
     hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-    if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
+    if (hl_out) hl_out[f] = (uint8_t)hl;
 }
 
 // ------------------------------ header-chain walk, many streams ------------------------------
@@ -1252,15 +1130,14 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 // ------------------------------ host launchers ------------------------------
 struct CopyWs {
     WsHead* head;
-    ScanState* states;  // right after the head: one zeroing launch covers both
-    uint64_t* ubase;
+    V2* tiles;  // ntiles + 1: tile prefixes, then the totals
+    V2* grp;    // one per 256-frame row: its prefix inside the tile
     UnitRec* rec;
     u32x4* edge;
 };
 
-static uint64_t n_scan_blocks(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
-// tiles of the fused scan + prologue (256 frames each): one tile state each
-static uint64_t n_copy_tiles(uint32_t n) { return ((uint64_t)n + kBlock - 1) / kBlock; }
+static uint64_t n_tiles(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
+static uint64_t n_rows(uint32_t n) { return ((uint64_t)n + kBlock - 1) / kBlock; }
 // sum of unit_bound(R_f) <= total / (16 U) + n (1 + 63 / U) (and total <= cap)
 // (rounded up to whole blocks: every wave of the copy grid reads its record)
 static uint64_t max_units(uint32_t n, uint64_t cap)
@@ -1272,70 +1149,64 @@ static uint64_t max_units(uint32_t n, uint64_t cap)
 static uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
 static uint64_t r256(uint64_t x) { return (x + 255) & ~255ull; }
 
+// head, tile prefixes, row prefixes (the scan's scratch)
+static size_t scan_ws_size(uint32_t n)
+{
+    return r16(sizeof(WsHead)) + (n_tiles(n) + 1) * sizeof(V2) + n_rows(n) * sizeof(V2);
+}
+static void carve_scan(char* p, uint32_t n, CopyWs& c)
+{
+    c.head = reinterpret_cast<WsHead*>(p);
+    c.tiles = reinterpret_cast<V2*>(p + r16(sizeof(WsHead)));
+    c.grp = c.tiles + n_tiles(n) + 1;
+}
+
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-    return r256(sizeof(WsHead) + r16((n_copy_tiles(n) + 1) * sizeof(ScanState)) + r16(((uint64_t)n + 1) * 8)) +
-           r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
+    return r256(scan_ws_size(n)) + r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
 {
     if (!ws || ws_bytes < copy_ws_size(n, cap)) return false;
     char* p = static_cast<char*>(ws);
-    c.head = reinterpret_cast<WsHead*>(p);
-    p += sizeof(WsHead);
-    c.states = reinterpret_cast<ScanState*>(p);
-    p += r16((n_copy_tiles(n) + 1) * sizeof(ScanState));
-    c.ubase = reinterpret_cast<uint64_t*>(p);
-    p += r16(((uint64_t)n + 1) * 8);
-    p = static_cast<char*>(ws) + r256(p - static_cast<char*>(ws));  // edge words and records on whole lines
+    carve_scan(p, n, c);
+    p += r256(scan_ws_size(n));  // edge words and records on whole lines
     c.edge = reinterpret_cast<u32x4*>(p);
     p += r256((uint64_t)n * kEdgeWords * 16);
     c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
 }
 
-// kmws_pack_headers: wire offsets -> out (n+1 entries) and the header slots;
-// also zeroes the workspace head (status, ticket) and tile states first.  Two
-// launches.
+// Zero the head (status), reduce_kernel, scan_tiles_kernel (n > 0).
 template <class Size>
-static kmws_status launch_scan(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s, u32x4* hdr = nullptr,
-                               uint8_t* hl_out = nullptr)
+static kmws_status launch_reduce(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s)
 {
-    const uint32_t nb = (uint32_t)n_scan_blocks(n);
-    if (nb == 0) {
-        if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        return launch_zero(out, sizeof(uint64_t), s);
-    }
-    const uint64_t words = (sizeof(WsHead) + (uint64_t)nb * sizeof(ScanState)) / 8;
-    const uint64_t zb = (words + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
-                       reinterpret_cast<uint64_t*>(c.head), words);
-    // (the unit-slot bases, the scan's second quantity, are not needed here: not written)
-    hipLaunchKernelGGL(scan_kernel<Size>, dim3(nb), dim3(kBlock), 0, s, size, n, nb, c.states, c.head, out,
-                       (uint64_t*)nullptr, hdr, hl_out);
+    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+    const uint32_t nt = (uint32_t)n_tiles(n);
+    hipLaunchKernelGGL(reduce_kernel<Size>, dim3(nt), dim3(kBlock), 0, s, size, n, c.tiles, c.grp);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(kBlock), 0, s, c.tiles, nt, out, n);
     return hip_status(hipGetLastError());
 }
 
-// Encode / gather: zero the head and the scan's tile states, the fused scan +
-// prologue (offsets, unit slot bases, edge words, unit records), the copy grid.
-// Three launches, stream-ordered, nothing on the host in between.
+// Encode / gather: zero the head, reduce (row and tile totals), scan the tile
+// totals, the prologue (offsets, edge words, unit records), the copy grid.
+// Five launches,
+// stream-ordered, nothing on the host in between.
 template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
                                const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     if (n == 0) {
         if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        if (launch_zero(start, sizeof(uint64_t), s) != KMWS_OK) return KMWS_ERR_FAILED;
-        return launch_zero(c.ubase, sizeof(uint64_t), s);
+        return launch_zero(start, sizeof(uint64_t), s);
     }
-    const uint32_t nt = (n + kBlock - 1) / kBlock;  // scan + prologue tiles (256 frames)
-    const uint64_t words = (sizeof(WsHead) + (uint64_t)nt * sizeof(ScanState)) / 8;
-    const uint64_t zb = (words + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
-                       reinterpret_cast<uint64_t*>(c.head), words);
-    hipLaunchKernelGGL(scan_prologue_kernel<HEADERS>, dim3(nt), dim3(kBlock), 0, s, src, d, flags, n, nt, cap,
-                       c.states, c.head, start, c.ubase, c.rec, c.edge);
+    const kmws_status st = HEADERS ? launch_reduce(WireSize{d, flags}, n, start, c, s)
+                                   : launch_reduce(PayloadSize{d}, n, start, c, s);
+    if (st != KMWS_OK) return st;
+    const uint32_t nt = (uint32_t)n_tiles(n);
+    hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
+                       c.head, c.tiles, nt, c.grp, start, c.rec, c.edge);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
     // concurrent DRAM streams; capped by 32 KiB of dynamic LDS per block),
     // batches of small frames need every wave slot to hide their per-unit
@@ -1347,8 +1218,7 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
     for (uint64_t u0 = 0; u0 < units; u0 += kMaxUnitsPerLaunch) {
         const uint64_t nu = units - u0 < kMaxUnitsPerLaunch ? units - u0 : kMaxUnitsPerLaunch;
         hipLaunchKernelGGL(copy_kernel<HEADERS>, dim3((uint32_t)((nu + kWavesPerBlock - 1) / kWavesPerBlock)),
-                           dim3(kBlock), lds_pad, s, src, dst, start, d, flags, n, c.ubase, c.rec, c.edge, c.head, u0,
-                           kCopySplit);
+                           dim3(kBlock), lds_pad, s, src, dst, c.tiles + nt, c.rec, c.edge, c.head, u0, kCopySplit);
     }
     return hip_status(hipGetLastError());
 }
@@ -1387,12 +1257,7 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
 
-// scan tile states + scratch unit bases after the status word (the scan's second
-// quantity is not needed here but costs nothing)
-size_t kmws_pack_headers_workspace_size(uint32_t n)
-{
-    return sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)) + r16(((uint64_t)n + 1) * 8);
-}
+size_t kmws_pack_headers_workspace_size(uint32_t n) { return scan_ws_size(n); }
 
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
                               uint8_t* hl_out, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
@@ -1402,21 +1267,22 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
     if ((n && (!descs || !flags || !hdr)) || (reinterpret_cast<uintptr_t>(hdr) & 15u) ||
         (wire_off && !workspace))
         return KMWS_ERR_INVALID_PARAM;
+    u32x4* h = reinterpret_cast<u32x4*>(hdr);
     if (wire_off) {
         if (workspace_bytes < kmws_pack_headers_workspace_size(n)) return KMWS_ERR_BUFFER_TOO_SMALL;
-        char* p = static_cast<char*>(workspace);
         CopyWs c;
-        c.head = reinterpret_cast<WsHead*>(p);
-        c.states = reinterpret_cast<ScanState*>(p + sizeof(WsHead));
-        c.ubase = reinterpret_cast<uint64_t*>(p + sizeof(WsHead) + r16((n_scan_blocks(n) + 1) * sizeof(V2)));
-        c.rec = nullptr;
-        c.edge = nullptr;
-        // the scan writes the header slots too
-        return launch_scan(WireSize{descs, flags}, n, wire_off, c, s, reinterpret_cast<u32x4*>(hdr), hl_out);
+        carve_scan(static_cast<char*>(workspace), n, c);
+        if (n == 0) return launch_zero(wire_off, sizeof(uint64_t), s);
+        // four launches: zero the head, reduce, scan the tiles, headers + offsets
+        const kmws_status st = launch_reduce(WireSize{descs, flags}, n, wire_off, c, s);
+        if (st != KMWS_OK) return st;
+        hipLaunchKernelGGL(pack_headers_kernel<true>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n,
+                           h, hl_out, c.tiles, c.grp, wire_off);
+        return hip_status(hipGetLastError());
     }
     if (n == 0) return KMWS_OK;
-    hipLaunchKernelGGL(pack_headers_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, descs, flags, n,
-                       reinterpret_cast<u32x4*>(hdr), hl_out);
+    hipLaunchKernelGGL(pack_headers_kernel<false>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n, h,
+                       hl_out, (const V2*)nullptr, (const V2*)nullptr, (uint64_t*)nullptr);
     return hip_status(hipGetLastError());
 }
 
