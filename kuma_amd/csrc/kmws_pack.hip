@@ -193,11 +193,13 @@ __device__ __forceinline__ V2 block_excl_scan(V2 v, V2* __restrict__ s_w, V2& to
 constexpr uint32_t kPastEnd = 1u << 31;  // SizeRaw.fl: a slot past the batch
 template <class Size>
 __global__ void __launch_bounds__(kBlock) reduce_kernel(Size size, uint32_t n, V2* __restrict__ tiles,
-                                                        V2* __restrict__ grp)
+                                                        V2* __restrict__ grp, WsHead* __restrict__ head)
 {
     __shared__ SizeRaw s_raw[kScanTile];
     __shared__ V2 s_row[kRowsPerTile];
     const uint32_t t = threadIdx.x;
+    // the batch's status word starts clear (set only by the kernels after this one)
+    if (blockIdx.x == 0 && t == 0) head->status = 0;
     const uint64_t F = (uint64_t)blockIdx.x * kScanTile;
     SizeRaw raw[kRowsPerTile];
 #pragma unroll
@@ -1178,20 +1180,18 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     return true;
 }
 
-// Zero the head (status), reduce_kernel, scan_tiles_kernel (n > 0).
+// reduce_kernel (which also clears the status word), scan_tiles_kernel (n > 0).
 template <class Size>
 static kmws_status launch_reduce(Size size, uint32_t n, uint64_t* out, CopyWs& c, hipStream_t s)
 {
-    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     const uint32_t nt = (uint32_t)n_tiles(n);
-    hipLaunchKernelGGL(reduce_kernel<Size>, dim3(nt), dim3(kBlock), 0, s, size, n, c.tiles, c.grp);
+    hipLaunchKernelGGL(reduce_kernel<Size>, dim3(nt), dim3(kBlock), 0, s, size, n, c.tiles, c.grp, c.head);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(kBlock), 0, s, c.tiles, nt, out, n);
     return hip_status(hipGetLastError());
 }
 
-// Encode / gather: zero the head, reduce (row and tile totals), scan the tile
-// totals, the prologue (offsets, edge words, unit records), the copy grid.
-// Five launches,
+// Encode / gather: reduce (row and tile totals), scan the tile totals, the
+// prologue (offsets, edge words, unit records), the copy grid.  Four launches,
 // stream-ordered, nothing on the host in between.
 template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
@@ -1273,7 +1273,7 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
         CopyWs c;
         carve_scan(static_cast<char*>(workspace), n, c);
         if (n == 0) return launch_zero(wire_off, sizeof(uint64_t), s);
-        // four launches: zero the head, reduce, scan the tiles, headers + offsets
+        // three launches: reduce, scan the tiles, headers + offsets
         const kmws_status st = launch_reduce(WireSize{descs, flags}, n, wire_off, c, s);
         if (st != KMWS_OK) return st;
         hipLaunchKernelGGL(pack_headers_kernel<true>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n,
