@@ -1010,34 +1010,210 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
 
 // ------------------------------ header pack only ------------------------------
 // One lane per frame: the header bytes of WSHandler::encodeFrameHeader in a
-// 16-byte slot (one coalesced store per lane) and its length; with OFFSETS
-// (after reduce_kernel) also the frame's wire offset, the row's prefix plus a
-// block scan.
-template <bool OFFSETS>
+// 16-byte slot (one coalesced store per lane) and its length (no wire offsets:
+// those come from pack_headers_chain_kernel below).
 __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* __restrict__ d,
                                                               const uint16_t* __restrict__ flags, uint32_t n,
-                                                              u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out,
-                                                              const V2* __restrict__ tiles,
-                                                              const V2* __restrict__ grp, uint64_t* __restrict__ out)
+                                                              u32x4* __restrict__ hdr, uint8_t* __restrict__ hl_out)
 {
-    __shared__ V2 s_w[kBlock / 64];
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = f < n;
-    const kmws_desc x = d[live ? f : n - 1];
-    const uint32_t fl = flags[live ? f : n - 1];
-    const uint32_t hl = hdr_len(x.len, (fl >> 8) & 1u);
-    if (OFFSETS) {
-        const V2 pre = tiles[blockIdx.x / kRowsPerTile] + grp[blockIdx.x];
-        V2 row;
-        const uint64_t r = (uint64_t)hl + x.len;
-        const V2 off = pre + block_excl_scan(live ? V2{r, 0} : V2{0, 0}, s_w, row);
-        if (live) out[f] = off.a;
-    }
-    if (!live) return;
+    if (f >= n) return;
+    const kmws_desc x = d[f];
+    const uint32_t fl = flags[f];
     uint64_t h0, h1;
     build_header(x.len, fl, x.key, h0, h1);
     hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-    if (hl_out) hl_out[f] = (uint8_t)hl;
+    if (hl_out) hl_out[f] = (uint8_t)hdr_len(x.len, (fl >> 8) & 1u);
+}
+
+// ------------------------------ header pack, one pass ------------------------------
+// kmws_pack_headers with wire offsets as ONE pass over the descriptors: a
+// chained scan (decoupled look-back) over 2048-frame tiles, tile = blockIdx.x.
+// A block loads its tile's descriptors once, writes the header slots at once,
+// publishes its tile's aggregate, resolves its prefix from its predecessors'
+// published states and writes the wire offsets.  The three-pass form (reduce,
+// scan the tile totals, emit) reads the descriptors twice and pays two kernel
+// boundaries (17-19 + 5 + 27 us on 4 M frames, r03w_pack_kernel_trace.txt).
+//
+// What the first look-back scan of this round (c527e0f, 95-115 us) did not
+// survive: tile tickets from ONE atomic counter (a word serves ~88 atomics per
+// us: 2048 tickets alone ~23 us, MI355X_MICROARCH.md "dequeue") and a 64-tile
+// window (late tiles walked 16-32 dependent steps).  Here the tile is the block
+// index -- a block waits only on lower-indexed blocks, which the dispatcher has
+// placed before it; the spin is bounded all the same (a state that never
+// arrives sets the status instead of hanging) -- and one look-back step reads
+// 512 states at once (two per thread of the block), so a tile resolves in one
+// or two latencies once its predecessors have published their aggregates.
+//
+// Tile state: one 64-bit word, value << 2 | flag (0 none, 1 aggregate, 2
+// inclusive prefix), written and read with agent-scope atomics (the XCDs' L2s
+// are not coherent for plain accesses); zeroed by a kernel before each call.
+constexpr int kLookK = 2;
+constexpr uint32_t kLookW = kBlock * kLookK;  // 512 tiles per look-back step
+constexpr uint64_t kStAgg = 1ull, kStInc = 2ull;
+constexpr uint32_t kLookSpinLimit = 1u << 20;
+
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, o, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+// The whole block: the exclusive prefix of tile `tile` (> 0).  Thread t, slot k
+// looks at the tile at distance t + 256 k below `base`; the states up to and
+// including the nearest inclusive one are summed (tiles below 0 count as an
+// inclusive zero); a window without one is summed whole and the next window
+// read.  (The other waves would only wait at the barrier; spreading the window
+// over them keeps the kernel at 8 blocks per CU: one wave reading 512 states
+// took 94 VGPRs.)  s_red: 8 words of LDS.
+__device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, WsHead* __restrict__ head,
+                              uint64_t* __restrict__ s_red)
+{
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t* s_dmin = reinterpret_cast<uint32_t*>(s_red);  // 4 words
+    uint64_t* s_sum = s_red + 4;                            // 4 words
+    uint64_t pre = 0;
+    uint32_t spins = 0;
+    for (int64_t base = (int64_t)tile - 1;; base -= kLookW) {
+        uint64_t v[kLookK];
+#pragma unroll
+        for (int k = 0; k < kLookK; ++k) {
+            const int64_t j = base - (int64_t)(t + kBlock * k);
+            v[k] = j >= 0 ? ld_agent(st + j) : kStInc;
+        }
+        for (;;) {
+            uint32_t dmin = kLookW;
+#pragma unroll
+            for (int k = kLookK - 1; k >= 0; --k)
+                if ((v[k] & 3u) == kStInc) dmin = t + kBlock * k;
+            dmin = wave_min_u32(dmin);
+            if (lane == 0) s_dmin[wave] = dmin;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) dmin = s_dmin[w] < dmin ? s_dmin[w] : dmin;
+            bool missing = false;
+#pragma unroll
+            for (int k = 0; k < kLookK; ++k) missing |= t + kBlock * k < dmin && (v[k] & 3u) == 0;
+            if (!__syncthreads_or(missing)) {
+                uint64_t s = 0;
+#pragma unroll
+                for (int k = 0; k < kLookK; ++k)
+                    if (t + kBlock * k <= dmin) s += v[k] >> 2;
+                s = wave_sum(s);
+                if (lane == 0) s_sum[wave] = s;
+                __syncthreads();
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) pre += s_sum[w];
+                if (dmin < kLookW) return pre;
+                break;  // the whole window was aggregates: the next one
+            }
+            if (++spins >= kLookSpinLimit) {  // cannot happen: every lower tile publishes
+                if (t == 0) atomicOr(&head->status, kStatusBadDesc);
+                return pre;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int k = 0; k < kLookK; ++k) {
+                const int64_t j = base - (int64_t)(t + kBlock * k);
+                if (j >= 0 && (v[k] & 3u) != kStInc) v[k] = ld_agent(st + j);
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) pack_headers_chain_kernel(const kmws_desc* __restrict__ d,
+                                                                    const uint16_t* __restrict__ flags, uint32_t n,
+                                                                    u32x4* __restrict__ hdr,
+                                                                    uint8_t* __restrict__ hl_out,
+                                                                    uint64_t* __restrict__ out,
+                                                                    uint64_t* __restrict__ st,
+                                                                    WsHead* __restrict__ head)
+{
+    __shared__ uint64_t s_sz[kScanTile];  // region sizes, then wire offsets
+    __shared__ uint64_t s_w[kBlock / 64];
+    __shared__ uint64_t s_red[8];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t F = (uint64_t)tile * kScanTile;
+    // frames F + i * 256 + t: every load and store coalesced, all loads issued at once
+    kmws_desc x[kScanItems];
+    uint32_t fl[kScanItems];
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        const uint32_t j = (uint32_t)__builtin_elementwise_min(f, (uint64_t)n - 1);
+        x[i] = d[j];
+        fl[i] = flags[j];
+    }
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        const uint32_t hl = hdr_len(x[i].len, (fl[i] >> 8) & 1u);
+        s_sz[i * kBlock + t] = f < n ? (uint64_t)hl + x[i].len : 0;
+        if (f < n) {  // the header slots need no offset: written before the look-back
+            uint64_t h0, h1;
+            build_header(x[i].len, fl[i], x[i].key, h0, h1);
+            hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
+            if (hl_out) hl_out[f] = (uint8_t)hl;
+        }
+    }
+    __syncthreads();
+    // thread t: frames 8t .. 8t + 7 of the tile (only thread t reads or writes
+    // these entries until the barrier before the stores)
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) sum += s_sz[kScanItems * t + k];
+    const uint64_t inc = wave_incl_scan(sum);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint64_t v = s_w[w];
+        if (w < (int)wave) before += v;
+        agg += v;
+    }
+    uint64_t pre = 0;
+    if (tile == 0) {
+        if (t == 0) st_agent(st, agg << 2 | kStInc);
+    } else {
+        if (t == 0) st_agent(st + tile, agg << 2 | kStAgg);
+        pre = look_back(st, tile, head, s_red);  // block-uniform
+        if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
+    }
+    if (t == 0 && F + kScanTile >= n) out[n] = pre + agg;  // the last tile: the total
+    uint64_t run = pre + before + inc - sum;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t r = s_sz[kScanItems * t + k];
+        s_sz[kScanItems * t + k] = run;
+        run += r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        if (f < n) out[f] = s_sz[i * kBlock + t];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict__ p, uint64_t words)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
+        p[i] = 0;
 }
 
 // ------------------------------ header-chain walk, many streams ------------------------------
@@ -1257,7 +1433,8 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
 
-size_t kmws_pack_headers_workspace_size(uint32_t n) { return scan_ws_size(n); }
+// head, then one 64-bit state per 2048-frame tile (pack_headers_chain_kernel)
+size_t kmws_pack_headers_workspace_size(uint32_t n) { return r16(sizeof(WsHead)) + n_tiles(n) * sizeof(uint64_t); }
 
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
                               uint8_t* hl_out, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
@@ -1270,19 +1447,23 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
     u32x4* h = reinterpret_cast<u32x4*>(hdr);
     if (wire_off) {
         if (workspace_bytes < kmws_pack_headers_workspace_size(n)) return KMWS_ERR_BUFFER_TOO_SMALL;
-        CopyWs c;
-        carve_scan(static_cast<char*>(workspace), n, c);
-        if (n == 0) return launch_zero(wire_off, sizeof(uint64_t), s);
-        // three launches: reduce, scan the tiles, headers + offsets
-        const kmws_status st = launch_reduce(WireSize{descs, flags}, n, wire_off, c, s);
-        if (st != KMWS_OK) return st;
-        hipLaunchKernelGGL(pack_headers_kernel<true>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n,
-                           h, hl_out, c.tiles, c.grp, wire_off);
+        WsHead* head = static_cast<WsHead*>(workspace);
+        uint64_t* st = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + r16(sizeof(WsHead)));
+        if (n == 0) {
+            if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+            return launch_zero(wire_off, sizeof(uint64_t), s);
+        }
+        // two launches: zero the head and the tile states, then the chained scan
+        const uint64_t words = kmws_pack_headers_workspace_size(n) / 8;
+        const uint64_t zb = (words + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
+                           reinterpret_cast<uint64_t*>(head), words);
+        hipLaunchKernelGGL(pack_headers_chain_kernel, dim3((uint32_t)n_tiles(n)), dim3(kBlock), 0, s, descs, flags, n, h,
+                           hl_out, wire_off, st, head);
         return hip_status(hipGetLastError());
     }
     if (n == 0) return KMWS_OK;
-    hipLaunchKernelGGL(pack_headers_kernel<false>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n, h,
-                       hl_out, (const V2*)nullptr, (const V2*)nullptr, (uint64_t*)nullptr);
+    hipLaunchKernelGGL(pack_headers_kernel, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, descs, flags, n, h, hl_out);
     return hip_status(hipGetLastError());
 }
 

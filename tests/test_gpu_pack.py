@@ -280,6 +280,64 @@ def test_pack_headers_parity(T, kind):
     assert T.equal(hdr2, hdr)
 
 
+def np_header_slots(lens, flags, keys):
+    """encodeFrameHeader (WSHandler.cpp:46-106) vectorised: (n, 16) zero-padded
+    slots and lengths.  Checked against the oracle's encode_header on a sample in
+    test_pack_headers_chain_many_tiles."""
+    n = len(lens)
+    L = lens.astype(np.int64)
+    m = ((flags >> 8) & 1).astype(np.int64)
+    cls = np.where(L <= 125, 0, np.where(L <= 0xFFFF, 1, 2))
+    S = np.zeros((n, 16), dtype=np.uint8)
+    S[:, 0] = flags & 0xFF
+    S[:, 1] = (m << 7) | np.where(cls == 0, L, np.where(cls == 1, 126, 127))
+    c1, c2 = cls == 1, cls == 2
+    S[c1, 2], S[c1, 3] = (L[c1] >> 8) & 0xFF, L[c1] & 0xFF
+    for k in range(4):  # 127 class: 4 zero bytes, then the 32-bit length big-endian
+        S[c2, 6 + k] = (L[c2] >> (8 * (3 - k))) & 0xFF
+    base = np.array([2, 4, 10])[cls]
+    rows = np.nonzero(m)[0]
+    for k in range(4):
+        S[rows, base[rows] + k] = (keys[rows].astype(np.int64) >> (8 * k)) & 0xFF
+    return S, (base + 4 * m).astype(np.uint8)
+
+
+@pytest.mark.parametrize("n", [2047, 2048, 2049, 6145, 1_500_001])
+def test_pack_headers_chain_many_tiles(T, n):
+    """The one-pass header pack over many 2048-frame tiles: 1.5 M frames = 733
+    tiles, more than one 512-tile look-back window.  Slots, lengths and wire
+    offsets == the vectorised encodeFrameHeader and the exclusive scan of
+    header + payload bytes (the oracle's encode_batch offsets), every frame;
+    the vectorised headers == the oracle's on a sample.  Repeated on the same
+    workspace (the tile states are re-zeroed per call)."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(n)
+    lens = rng.choice([0, 7, 125, 126, 4096, 65535, 65536, 70000, 10485760], size=n).astype(np.int64)
+    flags = (rng.integers(0, 256, size=n) | (rng.integers(0, 2, size=n) << 8)).astype(np.uint32)
+    keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    S, hl = np_header_slots(lens, flags, keys)
+    for i in list(rng.integers(0, n, size=64)) + [0, n - 1]:
+        want_h = orc.encode_header(orc.Hdr(fin=int(flags[i] >> 7 & 1), rsv1=int(flags[i] >> 6 & 1),
+                                           rsv2=int(flags[i] >> 5 & 1), rsv3=int(flags[i] >> 4 & 1),
+                                           opcode=int(flags[i] & 15), mask=int(flags[i] >> 8 & 1),
+                                           maskey=int(keys[i]).to_bytes(4, "little"), length=int(lens[i])))
+        assert bytes(S[i]) == want_h + bytes(16 - len(want_h)) and hl[i] == len(want_h), i
+    woff_want = np.concatenate([[0], np.cumsum(lens + hl.astype(np.int64))])
+    descs = kmws.make_descs(np.zeros(n, np.int64), lens, keys.astype(np.int64))
+    fl = T.from_numpy(flags.astype(np.int16)).cuda()
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    for rep in range(2):
+        hdr = T.full((16 * n,), 0xEE, dtype=T.uint8, device="cuda")
+        hlo = T.zeros(n, dtype=T.uint8, device="cuda")
+        woff = T.full((n + 1,), -1, dtype=T.int64, device="cuda")
+        kmws.pack_headers(descs, fl, hdr, hlo, woff, ws)
+        T.cuda.synchronize()
+        assert ws.status() == 0, rep
+        assert np.array_equal(hdr.cpu().numpy().reshape(n, 16), S), rep
+        assert np.array_equal(hlo.cpu().numpy(), hl), rep
+        assert np.array_equal(woff.cpu().numpy(), woff_want), rep
+
+
 def test_find_headers_streams_matches_host_walk(T):
     """kmws_find_headers_streams (one lane per stream) == kmws_find_headers on
     each stream: complete streams, streams cut mid-frame, a corrupted length,
