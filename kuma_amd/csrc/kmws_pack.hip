@@ -1029,27 +1029,35 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
 // ------------------------------ header pack, one pass ------------------------------
 // kmws_pack_headers with wire offsets as ONE pass over the descriptors: a
 // chained scan (decoupled look-back) over 2048-frame tiles, tile = blockIdx.x.
-// A block loads its tile's descriptors once, writes the header slots at once,
-// publishes its tile's aggregate, resolves its prefix from its predecessors'
-// published states and writes the wire offsets.  The three-pass form (reduce,
-// scan the tile totals, emit) reads the descriptors twice and pays two kernel
-// boundaries (17-19 + 5 + 27 us on 4 M frames, r03w_pack_kernel_trace.txt).
+// A block loads its tile's {len, key} and flags once, publishes its tile's
+// aggregate, writes the header slots, resolves its prefix from its
+// predecessors' published states and writes the wire offsets.  (The
+// three-pass form -- reduce, scan the tile totals, emit -- reads the
+// descriptors twice and pays two kernel boundaries: 17-19 + 5 + 27 us on 4 M
+// frames, r03w_pack_kernel_trace.txt.)
 //
-// What the first look-back scan of this round (c527e0f, 95-115 us) did not
-// survive: tile tickets from ONE atomic counter (a word serves ~88 atomics per
-// us: 2048 tickets alone ~23 us, MI355X_MICROARCH.md "dequeue") and a 64-tile
-// window (late tiles walked 16-32 dependent steps).  Here the tile is the block
-// index -- a block waits only on lower-indexed blocks, which the dispatcher has
-// placed before it; the spin is bounded all the same (a state that never
-// arrives sets the status instead of hanging) -- and one look-back step reads
-// 512 states at once (two per thread of the block), so a tile resolves in one
-// or two latencies once its predecessors have published their aggregates.
+// Measured on 4 M frames (2048 tiles; wall time of the call, kernel time in
+// brackets; profiles/r03ak_pack_headers_ab.txt): this kernel 46 us [38-41]; the
+// same without the dependency 34 us [28]; the aggregate published after the
+// header-slot stores (queued ahead of it in the in-order vector memory queue)
+// 53 us; the header slots written after the look-back 74 us; a one-wave
+// look-back at 94 VGPRs (5 blocks per CU) [52-56]; a persistent grid of 512
+// blocks taking tiles in order [44]; prefixes from per-64-tile group counters
+// instead of a chain [163] (every waiting block polled the same few words); the
+// round's first look-back scan (c527e0f: tiles from one atomic ticket counter,
+// which serves ~88 atomics per us -- MI355X_MICROARCH.md "dequeue" -- and a
+// 64-tile window) [95-115].  What remains of the dependency: a tile's prefix
+// needs every lower tile's loads, which land in any order across the ~12 us the
+// descriptor reads take, so the offset stores of most tiles wait for the last.
 //
 // Tile state: one 64-bit word, value << 2 | flag (0 none, 1 aggregate, 2
 // inclusive prefix), written and read with agent-scope atomics (the XCDs' L2s
-// are not coherent for plain accesses); zeroed by a kernel before each call.
-constexpr int kLookK = 2;
-constexpr uint32_t kLookW = kBlock * kLookK;  // 512 tiles per look-back step
+// are not coherent for plain accesses); zeroed by a kernel before each call.  A
+// block waits only on lower-indexed blocks, which the dispatcher placed before
+// it; the spin is bounded all the same (a state that never arrives sets the
+// status instead of hanging).
+constexpr int kLookK = 2;  // look-back states per thread (4: 55 vs 53 us, r03ai)
+constexpr uint32_t kLookW = kBlock * kLookK;  // tiles per look-back step (512)
 constexpr uint64_t kStAgg = 1ull, kStInc = 2ull;
 constexpr uint32_t kLookSpinLimit = 1u << 20;
 
@@ -1060,6 +1068,14 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS accesses,
+// not for its outstanding global stores (__syncthreads would wait for every
+// header-slot store of the tile first).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
@@ -1076,17 +1092,23 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
 // looks at the tile at distance t + 256 k below `base`; the states up to and
 // including the nearest inclusive one are summed (tiles below 0 count as an
 // inclusive zero); a window without one is summed whole and the next window
-// read.  (The other waves would only wait at the barrier; spreading the window
-// over them keeps the kernel at 8 blocks per CU: one wave reading 512 states
-// took 94 VGPRs.)  s_red: 8 words of LDS.
+// read.  s_red: 8 words of LDS.
 __device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, WsHead* __restrict__ head,
                               uint64_t* __restrict__ s_red)
 {
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint32_t* s_dmin = reinterpret_cast<uint32_t*>(s_red);  // 4 words
+    uint32_t* s_miss = s_dmin + 4;                          // 4 words
     uint64_t* s_sum = s_red + 4;                            // 4 words
     uint64_t pre = 0;
     uint32_t spins = 0;
+    // One lane polls the nearest predecessor first; the window is read once it
+    // has published (polling the whole window from every waiting block took
+    // bandwidth from the descriptor loads the states wait on).
+    if (t == 0) {
+        while ((ld_agent(st + tile - 1) & 3u) == 0 && ++spins < kLookSpinLimit) __builtin_amdgcn_s_sleep(8);
+    }
+    lds_barrier();
     for (int64_t base = (int64_t)tile - 1;; base -= kLookW) {
         uint64_t v[kLookK];
 #pragma unroll
@@ -1101,20 +1123,26 @@ __device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, Ws
                 if ((v[k] & 3u) == kStInc) dmin = t + kBlock * k;
             dmin = wave_min_u32(dmin);
             if (lane == 0) s_dmin[wave] = dmin;
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int w = 0; w < kBlock / 64; ++w) dmin = s_dmin[w] < dmin ? s_dmin[w] : dmin;
             bool missing = false;
 #pragma unroll
             for (int k = 0; k < kLookK; ++k) missing |= t + kBlock * k < dmin && (v[k] & 3u) == 0;
-            if (!__syncthreads_or(missing)) {
+            const uint32_t wm = __ballot(missing) != 0;
+            if (lane == 0) s_miss[wave] = wm;
+            lds_barrier();
+            uint32_t any_miss = 0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) any_miss |= s_miss[w];
+            if (!any_miss) {
                 uint64_t s = 0;
 #pragma unroll
                 for (int k = 0; k < kLookK; ++k)
                     if (t + kBlock * k <= dmin) s += v[k] >> 2;
                 s = wave_sum(s);
                 if (lane == 0) s_sum[wave] = s;
-                __syncthreads();
+                lds_barrier();
 #pragma unroll
                 for (int w = 0; w < kBlock / 64; ++w) pre += s_sum[w];
                 if (dmin < kLookW) return pre;
@@ -1124,53 +1152,85 @@ __device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, Ws
                 if (t == 0) atomicOr(&head->status, kStatusBadDesc);
                 return pre;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(8);
 #pragma unroll
-            for (int k = 0; k < kLookK; ++k) {
+            for (int k = 0; k < kLookK; ++k) {  // only the states still missing
                 const int64_t j = base - (int64_t)(t + kBlock * k);
-                if (j >= 0 && (v[k] & 3u) != kStInc) v[k] = ld_agent(st + j);
+                if (j >= 0 && t + kBlock * k < dmin && (v[k] & 3u) == 0) v[k] = ld_agent(st + j);
             }
         }
     }
 }
 
-__global__ void __launch_bounds__(kBlock) pack_headers_chain_kernel(const kmws_desc* __restrict__ d,
-                                                                    const uint16_t* __restrict__ flags, uint32_t n,
-                                                                    u32x4* __restrict__ hdr,
-                                                                    uint8_t* __restrict__ hl_out,
-                                                                    uint64_t* __restrict__ out,
-                                                                    uint64_t* __restrict__ st,
-                                                                    WsHead* __restrict__ head)
+// One block per tile (all 2048 tiles of 4 M frames resident at 8 blocks per
+// CU).  Measured (r03ah): a persistent form -- 512 blocks taking tiles b, b +
+// 512, ... in order with the next tile's loads in flight during the wait, so
+// that every tile's previous one is inclusive inside its window -- ran 44.4 us
+// of kernel against 38-41 us for this form (fewer loads in flight at 2 blocks
+// per CU: 40 us even without the dependency).
+__global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmws_desc* __restrict__ d,
+                                                                       const uint16_t* __restrict__ flags, uint32_t n,
+                                                                       u32x4* __restrict__ hdr,
+                                                                       uint8_t* __restrict__ hl_out,
+                                                                       uint64_t* __restrict__ out,
+                                                                       uint64_t* __restrict__ st,
+                                                                       WsHead* __restrict__ head)
 {
     __shared__ uint64_t s_sz[kScanTile];  // region sizes, then wire offsets
     __shared__ uint64_t s_w[kBlock / 64];
+    __shared__ uint64_t s_a[kBlock / 64];
     __shared__ uint64_t s_red[8];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t F = (uint64_t)tile * kScanTile;
     // frames F + i * 256 + t: every load and store coalesced, all loads issued at once
-    kmws_desc x[kScanItems];
+    // (only {len, key}, the descriptor's second 8 bytes, and the flags)
+    uint64_t lk[kScanItems];
     uint32_t fl[kScanItems];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         const uint64_t f = F + (uint64_t)i * kBlock + t;
         const uint32_t j = (uint32_t)__builtin_elementwise_min(f, (uint64_t)n - 1);
-        x[i] = d[j];
+        lk[i] = reinterpret_cast<const uint64_t*>(d + j)[1];
         fl[i] = flags[j];
     }
+    // the tile's aggregate first (a plain block sum: one barrier), published at once
+    uint64_t part = 0;
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         const uint64_t f = F + (uint64_t)i * kBlock + t;
-        const uint32_t hl = hdr_len(x[i].len, (fl[i] >> 8) & 1u);
-        s_sz[i * kBlock + t] = f < n ? (uint64_t)hl + x[i].len : 0;
-        if (f < n) {  // the header slots need no offset: written before the look-back
+        const uint32_t len = (uint32_t)lk[i];
+        part += f < n ? (uint64_t)hdr_len(len, (fl[i] >> 8) & 1u) + len : 0;
+    }
+    part = wave_sum(part);
+    if (lane == 0) s_a[wave] = part;
+    lds_barrier();
+    uint64_t agg = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) agg += s_a[w];
+#ifdef KMWS_AB_NO_LOOKBACK  // tuning build only (tools/ab_pack_headers.py): the kernel without its dependency
+    const bool first = true;
+#else
+    const bool first = tile == 0;
+#endif
+    if (t == 0) st_agent(st + tile, first ? agg << 2 | kStInc : agg << 2 | kStAgg);
+    // then the header slots (they need no offset; stores issued ahead of the
+    // publish would delay it: the vector memory queue is in order) and the sizes
+    // for the per-frame scan
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        const uint32_t len = (uint32_t)lk[i], key = (uint32_t)(lk[i] >> 32);
+        const uint32_t hl = hdr_len(len, (fl[i] >> 8) & 1u);
+        s_sz[i * kBlock + t] = f < n ? (uint64_t)hl + len : 0;
+        if (f < n) {
             uint64_t h0, h1;
-            build_header(x[i].len, fl[i], x[i].key, h0, h1);
+            build_header(len, fl[i], key, h0, h1);
             hdr[f] = u32x4{(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
             if (hl_out) hl_out[f] = (uint8_t)hl;
         }
     }
-    __syncthreads();
+    lds_barrier();
     // thread t: frames 8t .. 8t + 7 of the tile (only thread t reads or writes
     // these entries until the barrier before the stores)
     uint64_t sum = 0;
@@ -1178,19 +1238,13 @@ __global__ void __launch_bounds__(kBlock) pack_headers_chain_kernel(const kmws_d
     for (int k = 0; k < kScanItems; ++k) sum += s_sz[kScanItems * t + k];
     const uint64_t inc = wave_incl_scan(sum);
     if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    uint64_t before = 0, agg = 0;
+    lds_barrier();
+    uint64_t before = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) {
-        const uint64_t v = s_w[w];
-        if (w < (int)wave) before += v;
-        agg += v;
-    }
+    for (int w = 0; w < kBlock / 64; ++w)
+        if (w < (int)wave) before += s_w[w];
     uint64_t pre = 0;
-    if (tile == 0) {
-        if (t == 0) st_agent(st, agg << 2 | kStInc);
-    } else {
-        if (t == 0) st_agent(st + tile, agg << 2 | kStAgg);
+    if (!first) {
         pre = look_back(st, tile, head, s_red);  // block-uniform
         if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
     }
@@ -1202,7 +1256,7 @@ __global__ void __launch_bounds__(kBlock) pack_headers_chain_kernel(const kmws_d
         s_sz[kScanItems * t + k] = run;
         run += r;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         const uint64_t f = F + (uint64_t)i * kBlock + t;
@@ -1453,7 +1507,7 @@ kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uin
             if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
             return launch_zero(wire_off, sizeof(uint64_t), s);
         }
-        // two launches: zero the head and the tile states, then the chained scan
+        // two launches: zero the head and the tile states, then the one-pass kernel
         const uint64_t words = kmws_pack_headers_workspace_size(n) / 8;
         const uint64_t zb = (words + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
