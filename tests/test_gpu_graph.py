@@ -101,3 +101,52 @@ def test_graph_replay_encode_decode(T, n):
         g.replay()
         T.cuda.synchronize()
         check(src2, want2)
+
+
+def test_graph_replay_pack_headers(T):
+    """kmws_pack_headers with wire offsets (zero kernel + one-pass look-back
+    kernel over 2048-frame tiles) captured once and replayed on new lengths,
+    keys and flags written into the captured buffers: every replay's slots,
+    lengths and offsets equal the vectorised encodeFrameHeader and the exclusive
+    scan (the tile states are re-zeroed inside the graph)."""
+    from kuma_amd import kmws
+    from test_gpu_pack import np_header_slots
+    n = 300_001  # 147 tiles
+    dev = "cuda"
+    descs = T.zeros((n, 2), dtype=T.int64, device=dev)
+    fl = T.zeros(n, dtype=T.int16, device=dev)
+    hdr = T.zeros(16 * n, dtype=T.uint8, device=dev)
+    hl = T.zeros(n, dtype=T.uint8, device=dev)
+    woff = T.zeros(n + 1, dtype=T.int64, device=dev)
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+
+    def inputs(seed):
+        rng = np.random.default_rng(seed)
+        lens = rng.choice([0, 9, 125, 126, 4096, 65536, 200000], size=n).astype(np.int64)
+        flags = (rng.integers(0, 256, size=n) | (rng.integers(0, 2, size=n) << 8)).astype(np.uint32)
+        keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        descs.copy_(kmws.make_descs(np.zeros(n, np.int64), lens, keys.astype(np.int64)))
+        fl.copy_(T.from_numpy(flags.astype(np.int16)))
+        return lens, flags, keys
+
+    inputs(99)
+    s = T.cuda.Stream()
+    s.wait_stream(T.cuda.current_stream())
+    with T.cuda.stream(s):
+        kmws.pack_headers(descs, fl, hdr, hl, woff, ws)
+    T.cuda.current_stream().wait_stream(s)
+    T.cuda.synchronize()
+    g = T.cuda.CUDAGraph()
+    with T.cuda.graph(g):
+        kmws.pack_headers(descs, fl, hdr, hl, woff, ws)
+    T.cuda.synchronize()
+    for rep in range(3):
+        lens, flags, keys = inputs(rep)
+        woff.fill_(-1)
+        g.replay()
+        T.cuda.synchronize()
+        S, H = np_header_slots(lens, flags, keys)
+        assert ws.status() == 0, rep
+        assert np.array_equal(hdr.cpu().numpy().reshape(n, 16), S), rep
+        assert np.array_equal(hl.cpu().numpy(), H), rep
+        assert np.array_equal(woff.cpu().numpy(), np.concatenate([[0], np.cumsum(lens + H.astype(np.int64))])), rep
