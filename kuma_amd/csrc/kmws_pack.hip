@@ -87,8 +87,9 @@ __device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b +
 #define KMWS_UNIT_LANE_WORDS 4
 #endif
 // Output words per wave unit: 4 per lane (4 KiB).  2, 3, 5, 6 and 8 words per
-// lane measured the same or slower on cfg3/cfg4/64 KiB frames (within the
-// +-4 % run-to-run spread of one box; tools/gpu_ab_units.sh).
+// lane measured the same or slower on cfg3/cfg4/64 KiB frames (round 1); again
+// this round, 5 and 6 words per lane (one unit per 4 KiB fragment instead of
+// two): cfg4 encode 0.57 / 0.60 against 0.73 (profiles/r03aq_unit_words_ab.txt).
 constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
 #ifndef KMWS_COPY_SPLIT_DEFAULT
 #define KMWS_COPY_SPLIT_DEFAULT 8
