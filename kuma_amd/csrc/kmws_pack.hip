@@ -1037,19 +1037,22 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
 // descriptors twice and pays two kernel boundaries: 17-19 + 5 + 27 us on 4 M
 // frames, r03w_pack_kernel_trace.txt.)
 //
-// Measured on 4 M frames (2048 tiles; wall time of the call, kernel time in
-// brackets; profiles/r03ak_pack_headers_ab.txt): this kernel 46 us [38-41]; the
-// same without the dependency 34 us [28]; the aggregate published after the
-// header-slot stores (queued ahead of it in the in-order vector memory queue)
-// 53 us; the header slots written after the look-back 74 us; a one-wave
-// look-back at 94 VGPRs (5 blocks per CU) [52-56]; a persistent grid of 512
-// blocks taking tiles in order [44]; prefixes from per-64-tile group counters
-// instead of a chain [163] (every waiting block polled the same few words); the
-// round's first look-back scan (c527e0f: tiles from one atomic ticket counter,
-// which serves ~88 atomics per us -- MI355X_MICROARCH.md "dequeue" -- and a
-// 64-tile window) [95-115].  What remains of the dependency: a tile's prefix
-// needs every lower tile's loads, which land in any order across the ~12 us the
-// descriptor reads take, so the offset stores of most tiles wait for the last.
+// Measured on 4 M frames (2048 tiles; wall time per call, 20 calls back to
+// back; profiles/r03ak_pack_headers_ab.txt, r03ax_pack_headers_ab.txt): this
+// kernel 39.5-41 us; without the dependency 34 us (the floor of the design).
+// Per-tile timestamps (s_memrealtime) showed what the look-back costs: not the
+// wait itself but its reads -- every block reading a 512-tile window (two states
+// per thread) delayed the other tiles' descriptor loads (the last tile's loads
+// landed at 31.6 us instead of 20.9 without the dependency; 46-47 us per call),
+// a 256-tile window 44.5 us, this 64-tile window read by one wave, no block
+// barrier, 39.5-41 us (last loads at 22.9 us).  Also measured: the aggregate
+// published after the header-slot stores (queued ahead of it in the in-order
+// vector memory queue) 53 us; header slots after the look-back 74 us; a
+// persistent grid of 512 blocks taking tiles in order 50 us; prefixes from
+// per-64-tile group counters instead of a chain 169 us (every waiting block
+// polled the same few words); the round's first look-back scan (c527e0f: tiles
+// from one atomic ticket counter, which serves ~88 atomics per us --
+// MI355X_MICROARCH.md "dequeue" -- and a 64-tile window) 95-115 us of kernel.
 //
 // Tile state: one 64-bit word, value << 2 | flag (0 none, 1 aggregate, 2
 // inclusive prefix), written and read with agent-scope atomics (the XCDs' L2s
@@ -1057,8 +1060,6 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
 // block waits only on lower-indexed blocks, which the dispatcher placed before
 // it; the spin is bounded all the same (a state that never arrives sets the
 // status instead of hanging).
-constexpr int kLookK = 2;  // look-back states per thread (4: 55 vs 53 us, r03ai)
-constexpr uint32_t kLookW = kBlock * kLookK;  // tiles per look-back step (512)
 constexpr uint64_t kStAgg = 1ull, kStInc = 2ull;
 constexpr uint32_t kLookSpinLimit = 1u << 20;
 
@@ -1079,96 +1080,52 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t y = (uint32_t)__shfl_xor((int)x, o, 64);
-        x = y < x ? y : x;
-    }
-    return x;
-}
+#ifdef KMWS_AB_TRACE  // tuning build only: per-tile timestamps (s_memrealtime, 100 MHz) of the one-pass kernel
+constexpr int kTraceEv = 6;
+__device__ uint64_t g_trace[(1u << 16) * kTraceEv];
+#define KMWS_TRACE(tile, ev) \
+    do { if (threadIdx.x == 0 && (tile) < (1u << 16)) g_trace[(tile) * kTraceEv + (ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define KMWS_TRACE(tile, ev) do { } while (0)
+#endif
 
-// The whole block: the exclusive prefix of tile `tile` (> 0).  Thread t, slot k
-// looks at the tile at distance t + 256 k below `base`; the states up to and
-// including the nearest inclusive one are summed (tiles below 0 count as an
-// inclusive zero); a window without one is summed whole and the next window
-// read.  s_red: 8 words of LDS.
-__device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, WsHead* __restrict__ head,
-                              uint64_t* __restrict__ s_red)
+// One wave: the exclusive prefix of tile `tile` (> 0).  Lane 0 first polls the
+// nearest predecessor; then lane l looks at the tile at distance l below
+// `base`: the states up to and including the nearest inclusive one are summed
+// (tiles below 0 count as an inclusive zero), states still missing below it
+// are re-read alone; a 64-tile window of aggregates is summed whole and the
+// next one read.  No block barrier inside; the nearest inclusive state is
+// usually a few tiles away.
+__device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, WsHead* __restrict__ head)
 {
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint32_t* s_dmin = reinterpret_cast<uint32_t*>(s_red);  // 4 words
-    uint32_t* s_miss = s_dmin + 4;                          // 4 words
-    uint64_t* s_sum = s_red + 4;                            // 4 words
+    const uint32_t lane = threadIdx.x & 63;
     uint64_t pre = 0;
     uint32_t spins = 0;
-    // One lane polls the nearest predecessor first; the window is read once it
-    // has published (polling the whole window from every waiting block took
-    // bandwidth from the descriptor loads the states wait on).
-    if (t == 0) {
+    if (lane == 0) {
         while ((ld_agent(st + tile - 1) & 3u) == 0 && ++spins < kLookSpinLimit) __builtin_amdgcn_s_sleep(8);
     }
-    lds_barrier();
-    for (int64_t base = (int64_t)tile - 1;; base -= kLookW) {
-        uint64_t v[kLookK];
-#pragma unroll
-        for (int k = 0; k < kLookK; ++k) {
-            const int64_t j = base - (int64_t)(t + kBlock * k);
-            v[k] = j >= 0 ? ld_agent(st + j) : kStInc;
-        }
+    for (int64_t base = (int64_t)tile - 1;; base -= 64) {
+        const int64_t j = base - (int64_t)lane;
+        uint64_t v = j >= 0 ? ld_agent(st + j) : kStInc;
         for (;;) {
-            uint32_t dmin = kLookW;
-#pragma unroll
-            for (int k = kLookK - 1; k >= 0; --k)
-                if ((v[k] & 3u) == kStInc) dmin = t + kBlock * k;
-            dmin = wave_min_u32(dmin);
-            if (lane == 0) s_dmin[wave] = dmin;
-            lds_barrier();
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) dmin = s_dmin[w] < dmin ? s_dmin[w] : dmin;
-            bool missing = false;
-#pragma unroll
-            for (int k = 0; k < kLookK; ++k) missing |= t + kBlock * k < dmin && (v[k] & 3u) == 0;
-            const uint32_t wm = __ballot(missing) != 0;
-            if (lane == 0) s_miss[wave] = wm;
-            lds_barrier();
-            uint32_t any_miss = 0;
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) any_miss |= s_miss[w];
-            if (!any_miss) {
-                uint64_t s = 0;
-#pragma unroll
-                for (int k = 0; k < kLookK; ++k)
-                    if (t + kBlock * k <= dmin) s += v[k] >> 2;
-                s = wave_sum(s);
-                if (lane == 0) s_sum[wave] = s;
-                lds_barrier();
-#pragma unroll
-                for (int w = 0; w < kBlock / 64; ++w) pre += s_sum[w];
-                if (dmin < kLookW) return pre;
-                break;  // the whole window was aggregates: the next one
+            const uint64_t inc = __ballot((v & 3u) == kStInc);
+            const uint32_t dmin = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+            const bool missing = lane < dmin && (v & 3u) == 0;
+            if (__ballot(missing) == 0) {
+                pre += wave_sum(lane <= dmin ? v >> 2 : 0);
+                if (dmin < 64) return pre;
+                break;
             }
             if (++spins >= kLookSpinLimit) {  // cannot happen: every lower tile publishes
-                if (t == 0) atomicOr(&head->status, kStatusBadDesc);
+                if (lane == 0) atomicOr(&head->status, kStatusBadDesc);
                 return pre;
             }
             __builtin_amdgcn_s_sleep(8);
-#pragma unroll
-            for (int k = 0; k < kLookK; ++k) {  // only the states still missing
-                const int64_t j = base - (int64_t)(t + kBlock * k);
-                if (j >= 0 && t + kBlock * k < dmin && (v[k] & 3u) == 0) v[k] = ld_agent(st + j);
-            }
+            if (missing) v = ld_agent(st + j);
         }
     }
 }
 
-// One block per tile (all 2048 tiles of 4 M frames resident at 8 blocks per
-// CU).  Measured (r03ah): a persistent form -- 512 blocks taking tiles b, b +
-// 512, ... in order with the next tile's loads in flight during the wait, so
-// that every tile's previous one is inclusive inside its window -- ran 44.4 us
-// of kernel against 38-41 us for this form (fewer loads in flight at 2 blocks
-// per CU: 40 us even without the dependency).
 __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmws_desc* __restrict__ d,
                                                                        const uint16_t* __restrict__ flags, uint32_t n,
                                                                        u32x4* __restrict__ hdr,
@@ -1180,10 +1137,11 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
     __shared__ uint64_t s_sz[kScanTile];  // region sizes, then wire offsets
     __shared__ uint64_t s_w[kBlock / 64];
     __shared__ uint64_t s_a[kBlock / 64];
-    __shared__ uint64_t s_red[8];
+    __shared__ uint64_t s_pre;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t F = (uint64_t)tile * kScanTile;
+    KMWS_TRACE(tile, 0);
     // frames F + i * 256 + t: every load and store coalesced, all loads issued at once
     // (only {len, key}, the descriptor's second 8 bytes, and the flags)
     uint64_t lk[kScanItems];
@@ -1214,6 +1172,7 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
 #else
     const bool first = tile == 0;
 #endif
+    KMWS_TRACE(tile, 1);
     if (t == 0) st_agent(st + tile, first ? agg << 2 | kStInc : agg << 2 | kStAgg);
     // then the header slots (they need no offset; stores issued ahead of the
     // publish would delay it: the vector memory queue is in order) and the sizes
@@ -1246,7 +1205,14 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
         if (w < (int)wave) before += s_w[w];
     uint64_t pre = 0;
     if (!first) {
-        pre = look_back(st, tile, head, s_red);  // block-uniform
+        KMWS_TRACE(tile, 2);
+        if (wave == 0) {
+            const uint64_t p = look_back(st, tile, head);
+            if (lane == 0) s_pre = p;
+        }
+        lds_barrier();
+        pre = s_pre;
+        KMWS_TRACE(tile, 4);
         if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
     }
     if (t == 0 && F + kScanTile >= n) out[n] = pre + agg;  // the last tile: the total
@@ -1263,6 +1229,7 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
         const uint64_t f = F + (uint64_t)i * kBlock + t;
         if (f < n) out[f] = s_sz[i * kBlock + t];
     }
+    KMWS_TRACE(tile, 5);
 }
 
 __global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict__ p, uint64_t words)
@@ -1489,6 +1456,12 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
 }
 
 // head, then one 64-bit state per 2048-frame tile (pack_headers_chain_kernel)
+#ifdef KMWS_AB_TRACE
+int kmws_ab_trace_read(uint64_t* host, size_t n_words)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), n_words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 size_t kmws_pack_headers_workspace_size(uint32_t n) { return r16(sizeof(WsHead)) + n_tiles(n) * sizeof(uint64_t); }
 
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,

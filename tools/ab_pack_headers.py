@@ -43,8 +43,24 @@ def main():
         ts.append(e0.elapsed_time(e1) * 1e3)
     ts.sort()
     med = ts[len(ts) // 2]
-    print(json.dumps({"lib": sys.argv[1], "frames": n, "us_median": med, "us_min": ts[0],
-                      "hbm_frac": 43 * n / (med * 1e-6) / 8e12, "offsets_ok": ok}))
+    rec = {"lib": sys.argv[1], "frames": n, "us_median": med, "us_min": ts[0],
+           "hbm_frac": 43 * n / (med * 1e-6) / 8e12, "offsets_ok": ok}
+    if hasattr(L, "kmws_ab_trace_read"):  # tracing build: per-tile event times of one more call, us from the first start
+        call()
+        torch.cuda.synchronize()
+        nt = (n + 2047) // 2048
+        buf = np.zeros((1 << 16) * 6, dtype=np.uint64)
+        L.kmws_ab_trace_read.argtypes = [C.c_void_p, C.c_size_t]
+        assert L.kmws_ab_trace_read(buf.ctypes.data, buf.size) == 0
+        ev = buf[:nt * 6].reshape(nt, 6).astype(np.float64)
+        ev = (ev - ev[:, 0].min()) / 100.0  # s_memrealtime ticks at 100 MHz -> us
+        names = ["start", "aggregate", "published", "pred_seen", "resolved", "end"]
+        rec["trace_us"] = {nm: [round(float(np.percentile(ev[1:, k], q)), 2) for q in (0, 10, 50, 90, 100)]
+                           for k, nm in enumerate(names)}
+        rec["trace_note"] = "percentiles 0/10/50/90/100 over tiles 1.. of each event time"
+        idx = np.argsort(ev[:, 1])[-5:]
+        rec["last_aggregates"] = [[int(i), round(float(ev[i, 1]), 2)] for i in idx]
+    print(json.dumps(rec))
 
 
 if __name__ == "__main__":
