@@ -526,6 +526,13 @@ struct FrameUnits {
 // stored by the copy waves, which clip at the total.  Also the capacity check
 // (status set if the output exceeds cap; nothing is written then).
 //
+#ifdef KMWS_AB_TRACE_PRO  // tuning build only: per-block timestamps (s_memrealtime, 100 MHz) of the prologue
+__device__ uint64_t g_trace_pro[(1u << 16) * 8];
+#define KMWS_TRACE_PRO(ev) \
+    do { if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) g_trace_pro[blockIdx.x * 8 + (ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define KMWS_TRACE_PRO(ev) do { } while (0)
+#endif
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
                                                           const kmws_desc* __restrict__ d,
@@ -541,6 +548,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
     __shared__ uint8_t s_ne[kBlock];  // live edge words per frame
     __shared__ V2 s_w[kBlock / 64];
     const uint32_t t = threadIdx.x;
+    KMWS_TRACE_PRO(0);
     const uint64_t F0 = (uint64_t)blockIdx.x * kBlock;
     const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
     const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
@@ -556,6 +564,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
     const uint64_t rsz = (uint64_t)(HEADERS ? hdr_len(x[0].len, (fl[0] >> 8) & 1u) : 0u) + x[0].len;
     const V2 off = pre + block_excl_scan(t < nf ? V2{rsz, unit_bound(rsz)} : V2{0, 0}, s_w, row);
     const uint64_t r0 = off.a, uf = off.b, S0 = pre.b, uend = pre.b + row.b;
+    KMWS_TRACE_PRO(1);
     if (t < nf) start[f] = r0;
     if (total > cap) {  // records would not fit the workspace; the copy waves see the status (block-uniform)
         if (F0 == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
@@ -610,6 +619,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
             k = k < wlo ? wlo : (k > whi ? whi : k);
             S[j] = *reinterpret_cast<const u32x4*>(src + (nlive ? 16 * (uint64_t)k : 0));
         }
+        KMWS_TRACE_PRO(2);
         u32x4* my = s_edge + t * kEdgeWords;
         uint32_t third = 0;
         if (head_f && nedge) {
@@ -658,6 +668,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         }
     }
     __syncthreads();
+    KMWS_TRACE_PRO(3);
     // edge words of the block's frames: one contiguous run, whole 128-byte lines
     // (the run starts on one: 256 frames x 80 B), skipping lines without a live
     // word (a line written in part costs more than writing it whole)
@@ -672,6 +683,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         if (j0 + 2 < nf && j0 + 2 <= j1) live |= s_ne[j0 + 2] != 0;
         if (live) eout[i] = s_edge[i];  // dead words of a live line: any value (never read)
     }
+    KMWS_TRACE_PRO(4);
     // unit records, slot-parallel
     const uint32_t ns = s_ub[nf];
     for (uint32_t sl = t; sl < ns; sl += kBlock) {
@@ -704,6 +716,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         }
         rec[S0 + sl] = r;
     }
+    KMWS_TRACE_PRO(5);
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
@@ -1456,6 +1469,12 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
 }
 
 // head, then one 64-bit state per 2048-frame tile (pack_headers_chain_kernel)
+#ifdef KMWS_AB_TRACE_PRO
+int kmws_ab_trace_pro_read(uint64_t* host, size_t n_words)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_pro), n_words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef KMWS_AB_TRACE
 int kmws_ab_trace_read(uint64_t* host, size_t n_words)
 {

@@ -29,6 +29,7 @@ def main():
     import torch
     import bench_configs as bc
     libs = {"lib": bind(sys.argv[1])}
+    L0 = libs["lib"]
 
     def make_descs(off, length, key):
         off = torch.as_tensor(off, dtype=torch.int64)
@@ -88,6 +89,23 @@ def main():
                 tg = bc.timed(torch, gat, 5)
                 res.setdefault(name, []).append({"enc_frac": (2 * P + H) / te / 8e12,
                                                  "gat_frac": (2 * P) / tg / 8e12})
+        if hasattr(L0, "kmws_ab_trace_pro_read"):  # tracing build: prologue phases of one more encode / gather
+            for name, (enc, gat, _) in wires.items():
+                for label, fn in (("enc", enc), ("gat", gat)):
+                    fn()
+                    torch.cuda.synchronize()
+                    buf = np.zeros((1 << 16) * 8, dtype=np.uint64)
+                    L0.kmws_ab_trace_pro_read.argtypes = [C.c_void_p, C.c_size_t]
+                    assert L0.kmws_ab_trace_pro_read(buf.ctypes.data, buf.size) == 0
+                    nb = min((n + 255) // 256, 1 << 16)
+                    ev = buf[:nb * 8].reshape(nb, 8)[:, :6].astype(np.float64)
+                    ev = (ev - ev[:, 0].min()) / 100.0  # us from the first block's start
+                    ph = ["start", "scan", "src_loaded", "composed", "edges_out", "end"]
+                    res[f"trace_{label}"] = {p_: [round(float(np.percentile(ev[:, k], q)), 2) for q in (0, 10, 50, 90, 100)]
+                                             for k, p_ in enumerate(ph)}
+                    d = np.diff(ev, axis=1)
+                    res[f"phase_us_{label}"] = {f"{ph[k]}->{ph[k+1]}": [round(float(np.percentile(d[:, k], q)), 2)
+                                                                         for q in (50, 90, 100)] for k in range(5)}
         out[cfg] = res
         del wires, src, descs
         torch.cuda.empty_cache()
