@@ -308,9 +308,12 @@ size_t kmws_pack_headers_workspace_size(uint32_t n);
  * not touched: mask them in place with kmws_unmask_batch (XOR is its own
  * inverse), as sendWsFrame masks the caller's buffer (:388), on descriptors
  * whose key is 0 for every frame whose flags clear KMWS_FLAG_MASK (the header
- * then says unmasked; a nonzero key there would still be applied).  wire_off (n+1 entries, may be NULL) receives the offsets the
- * frames would have back to back on the wire (exclusive scan of header +
- * payload bytes) and the total in wire_off[n].  hdr 16-B aligned. */
+ * then says unmasked; a nonzero key there would still be applied).  wire_off
+ * (n+1 entries, may be NULL) receives the offsets the frames would have back
+ * to back on the wire (exclusive scan of header + payload bytes) and the total
+ * in wire_off[n]; it needs the workspace (a status word and one 8-byte scan
+ * state per 2048 frames, cleared by the call; one pass over the descriptors).
+ * hdr 16-B aligned. */
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
                               uint8_t* hdr_len, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
                               void* stream);
