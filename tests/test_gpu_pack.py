@@ -401,3 +401,53 @@ def test_find_headers_streams_matches_host_walk(T):
             i += 1
     assert i == len(hl)
     assert ends  # some complete streams were checked
+
+
+@pytest.mark.parametrize("n", [0, 1])
+def test_batch_entries_empty_and_single(T, n):
+    """0 and 1 frames through every device batch entry of the pack path:
+    kmws_pack_headers (one-pass offsets), kmws_encode_batch, kmws_unpack_headers
+    and kmws_gather_unmask.  Empty batches write wire_off[0] = 0 and a clear
+    status; a single frame equals the oracle (WSHandler.cpp:46-106, 303-310)."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(77 + n)
+    lens = np.array([70000], np.int64)[:n]
+    flags = np.array([0x182], np.uint32)[:n]           # FIN | BINARY, masked
+    keys = np.array([0x3D21FA37], np.uint32)[:n]
+    src = rng.integers(0, 256, size=70016 + 64, dtype=np.uint8)
+    offs = np.array([16], np.uint64)[:n]
+    want, want_off = orc.encode_batch(src, offs, lens, flags, keys) if n else (np.zeros(0, np.uint8), np.zeros(0))
+    total = len(want)
+    descs = kmws.make_descs(offs.astype(np.int64), lens, keys.astype(np.int64)).reshape(n, 2)
+    fl = T.from_numpy(flags.astype(np.int16)).cuda()
+    # header-only pack with offsets
+    hdr = T.zeros(16 * max(n, 1), dtype=T.uint8, device="cuda")
+    woff = T.full((n + 1,), -1, dtype=T.int64, device="cuda")
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    kmws.pack_headers(descs, fl, hdr, None, woff, ws)
+    T.cuda.synchronize()
+    assert ws.status() == 0 and int(woff[n]) == total
+    if n:
+        assert int(woff[0]) == 0 and bytes(hdr.cpu().numpy()[:len(want) - int(lens[0])]) == bytes(want[:len(want) - int(lens[0])])
+    # encode
+    wire = T.full((total + 16,), 0xEE, dtype=T.uint8, device="cuda")
+    wire_off = T.full((n + 1,), -1, dtype=T.int64, device="cuda")
+    ws_e = kmws.Workspace(kmws.copy_workspace_size(n, total + 16))
+    kmws.encode_batch(to_dev(T, src), descs, fl, wire, wire_off, ws_e)
+    T.cuda.synchronize()
+    assert ws_e.status() == 0 and int(wire_off[n]) == total
+    assert bytes(wire.cpu().numpy()[:total]) == bytes(want)
+    # unpack + gather back
+    out_desc = T.zeros((n, 2), dtype=T.int64, device="cuda")
+    out_err = T.full((max(n, 1),), 99, dtype=T.uint8, device="cuda")
+    ws_u = kmws.Workspace(kmws.lib().kmws_unpack_workspace_size())
+    kmws.unpack_headers(wire, wire_off[:n], kmws.SERVER, out_desc, None, out_err[:n], ws_u, wire_len=total)
+    dense = T.zeros(int(lens.sum()) + 16, dtype=T.uint8, device="cuda")
+    doff = T.full((n + 1,), -1, dtype=T.int64, device="cuda")
+    ws_g = kmws.Workspace(kmws.copy_workspace_size(n, dense.numel()))
+    kmws.gather_unmask(wire, out_desc, dense, doff, ws_g)
+    T.cuda.synchronize()
+    assert ws_u.status() == 0 and ws_g.status() == 0 and int(doff[n]) == int(lens.sum())
+    if n:
+        assert int(out_err[0]) == 0
+        assert bytes(dense.cpu().numpy()[:int(lens[0])]) == bytes(src[16:16 + int(lens[0])])
