@@ -150,3 +150,45 @@ def test_graph_replay_pack_headers(T):
         assert np.array_equal(hdr.cpu().numpy().reshape(n, 16), S), rep
         assert np.array_equal(hl.cpu().numpy(), H), rep
         assert np.array_equal(woff.cpu().numpy(), np.concatenate([[0], np.cumsum(lens + H.astype(np.int64))])), rep
+
+
+def test_pack_headers_beside_a_streaming_kernel(T):
+    """The one-pass header pack's blocks wait on lower-indexed blocks only, so it
+    completes (and is exact) while another stream keeps the CUs busy: a 4 GiB
+    in-place unmask runs on a second stream during three pack_headers calls of
+    1 M frames (512 tiles, more than one block per CU)."""
+    from kuma_amd import kmws
+    from test_gpu_pack import np_header_slots
+    n = 1 << 20
+    rng = np.random.default_rng(5)
+    lens = rng.choice([0, 5, 126, 4096, 70000], size=n).astype(np.int64)
+    flags = (rng.integers(0, 256, size=n) | (1 << 8)).astype(np.uint32)
+    keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    descs = kmws.make_descs(np.zeros(n, np.int64), lens, keys.astype(np.int64))
+    fl = T.from_numpy(flags.astype(np.int16)).cuda()
+    hdr = T.zeros(16 * n, dtype=T.uint8, device="cuda")
+    woff = T.zeros(n + 1, dtype=T.int64, device="cuda")
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    L = 65536
+    m = (4 << 30) // L
+    big = T.empty(m * L, dtype=T.uint8, device="cuda")
+    kmws.fill_synthetic(big, 11)
+    bdesc = T.empty((m, 2), dtype=T.int64, device="cuda")
+    kmws.fill_uniform_descs(bdesc, L, L, 12)
+    wsb = kmws.Workspace(kmws.unmask_workspace_size(m * L))
+    T.cuda.synchronize()
+    side = T.cuda.Stream()
+    with T.cuda.stream(side):
+        for _ in range(6):  # even: the batch ends masked, as generated
+            kmws.unmask_batch(big, bdesc, wsb, m * L)
+    for _ in range(3):
+        woff.fill_(-1)
+        kmws.pack_headers(descs, fl, hdr, None, woff, ws)
+    T.cuda.synchronize()
+    S, H = np_header_slots(lens, flags, keys)
+    assert ws.status() == 0 and wsb.status() == 0
+    assert np.array_equal(hdr.cpu().numpy().reshape(n, 16), S)
+    assert np.array_equal(woff.cpu().numpy(), np.concatenate([[0], np.cumsum(lens + H.astype(np.int64))]))
+    kmws.unmask_batch(big, bdesc, wsb, m * L)
+    T.cuda.synchronize()
+    assert kmws.check_unmasked(big, 11, bdesc) == 0
