@@ -434,13 +434,29 @@ def launch_ranks(n: int) -> int:
     never touches the GPU (it only forks children, no exec from a GPU process).
     Rank 0 prints the JSON line; returns the first non-zero exit status."""
     import subprocess
+    import threading
     port = _free_port()
-    procs = []
+    procs, pumps = [], []
+
+    def pump(r, stream):
+        # only rank 0's JSON line goes to stdout (the contract's ONE line); anything
+        # else the ranks or their libraries print (gloo's connection notices) to stderr
+        for line in stream:
+            out = sys.stdout if (r == 0 and line.startswith("{")) else sys.stderr
+            out.write(line)
+            out.flush()
+
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             stdout=subprocess.PIPE, text=True, bufsize=1)
+        procs.append(p)
+        pumps.append(threading.Thread(target=pump, args=(r, p.stdout), daemon=True))
+        pumps[-1].start()
     codes = [p.wait() for p in procs]
+    for t in pumps:
+        t.join()
     bad = [c for c in codes if c != 0]
     if bad:
         print(f"bench: rank exit codes {codes}", file=sys.stderr)

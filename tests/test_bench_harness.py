@@ -127,7 +127,11 @@ def test_launch_ranks_environment(tmp_path):
     r = subprocess.run([sys.executable, str(script), "--x", "1"], capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode == 0, r.stderr
-    rows = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    # only rank 0's JSON line reaches stdout (the contract's one line); the other
+    # ranks' output is forwarded to stderr
+    out = r.stdout.strip().splitlines()
+    assert len(out) == 1 and json.loads(out[0])["RANK"] == "0", r.stdout
+    rows = [json.loads(x) for x in out + [y for y in r.stderr.splitlines() if y.startswith("{")]]
     assert sorted(int(x["RANK"]) for x in rows) == [0, 1, 2]
     assert all(x["RANK"] == x["LOCAL_RANK"] and x["WORLD_SIZE"] == "3" and x["MASTER_ADDR"] == "127.0.0.1"
                for x in rows)

@@ -23,7 +23,9 @@ def run_bench(*args, timeout=300):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
                        timeout=timeout, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout[-2000:]  # ONE JSON line, whatever the ranks' libraries print
+    return json.loads(lines[0])
 
 
 @pytest.mark.parametrize("job,max_batch", [(65536, 16384), (50001, 20000)])
