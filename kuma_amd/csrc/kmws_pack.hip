@@ -92,8 +92,8 @@ __device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b +
 // two): cfg4 encode 0.57 / 0.60 against 0.73 (profiles/r03aq_unit_words_ab.txt).
 constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
 #ifndef KMWS_COPY_SPLIT_DEFAULT
-#define KMWS_COPY_SPLIT_DEFAULT 8
-#endif
+#define KMWS_COPY_SPLIT_DEFAULT 8  // re-measured on plain allocations this round: 2 / 4 / 16 / XCD runs all slower
+#endif                              // on cfg4 and cfg3 (profiles/r03bi_copy_split_ab.txt)
 constexpr uint32_t kCopySplit = KMWS_COPY_SPLIT_DEFAULT;
 constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
 #ifndef KMWS_LINE_BYTES
