@@ -55,7 +55,8 @@ def parse():
                    help="pin an unmask schedule code (include/kmws_gpu.h KMWS_SCHED_*); -1 = autotune the batch")
     p.add_argument("--seed", type=int, default=0x6B756D61)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core os.sched_getaffinity grants")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = the effective core count: os.sched_getaffinity capped by the cgroup CPU quota")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--no-autotune", action="store_true", help="skip kmws_unmask_autotune (keep the default schedule)")
     p.add_argument("--no-plain", action="store_true",
@@ -87,11 +88,33 @@ def host_cores():
     return aff, quota
 
 
+def effective_cores() -> int:
+    """Threads the host can actually run at once: the affinity set, capped by
+    the cgroup CPU quota rounded up (256 affinity cores under a 16-core quota
+    time-slice onto 16 cores' worth of CPU)."""
+    import math
+    aff, quota = host_cores()
+    return max(1, min(aff, math.ceil(quota))) if quota else aff
+
+
+def _time_unmask(orc, base, descs, threads: int, seconds: float):
+    orc.unmask_batch(base, descs, threads)  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        orc.unmask_batch(base, descs, threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return passes, el
+
+
 def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
     """Times the oracle (kuma's byte loop, WSHandler.cpp:303-310, restated in
     oracle/kmws_oracle.c) on host cores over a bounded sample of the same
-    workload: 16384 x frame_len frames (1 GiB), repeated for ~`seconds`, one
-    thread per core (SURVEY 8 d: kuma's loop on all host cores)."""
+    workload: 16384 x frame_len frames (1 GiB), repeated for ~`seconds` in
+    all: ~3/4 of it on `threads` threads (the effective core count: affinity
+    capped by the cgroup quota), the rest on one thread (SURVEY sec.6 quotes
+    kuma per core)."""
     import numpy as np
     from oracle import oracle as orc
     n = 16384  # 1 GiB of 64 KiB frames: 4x the host's L3, so the sample streams from DRAM
@@ -101,21 +124,19 @@ def cpu_baseline(seconds: float, threads: int, frame_len: int, seed: int):
     descs["off"] = np.arange(n, dtype=np.uint64) * frame_len
     descs["len"] = frame_len
     descs["key"] = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
-    orc.unmask_batch(base, descs, threads)  # warm
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        orc.unmask_batch(base, descs, threads)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    gib = passes * n * frame_len / 2**30
+    passes, el = _time_unmask(orc, base, descs, threads, seconds * 0.75)
+    p1, el1 = _time_unmask(orc, base, descs, 1, seconds * 0.25)
+    gib = n * frame_len / 2**30
     aff, quota = host_cores()
-    return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(passes * gib / el, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_core_GiB_s": round(p1 * gib / el1, 3),
             "affinity_cores": aff, "cgroup_cpu_quota_cores": quota,
             "sample": f"{n} x {frame_len} B frames ({n * frame_len >> 20} MiB), in-place unmask with the "
                       f"oracle's restatement of WSHandler::handleDataMask (scalar byte loop, gcc -O3), "
-                      f"{threads} threads, {passes} passes in {el:.1f} s",
+                      f"{threads} threads (affinity {aff} capped by the cgroup quota {quota}), {passes} passes "
+                      f"in {el:.1f} s; 1 thread: {p1} passes in {el1:.1f} s. The port is not calibrated "
+                      f"against a build of kuma's own src/ws: none is possible here (WSHandler.cpp needs "
+                      f"libkev headers the reference does not carry; DESIGN.md sec.2)",
             "cpu_model": _cpu_model()}
 
 
@@ -493,7 +514,7 @@ def plain_rate(kmws, torch, dev, n, L, descs, ws, schedule, seed, steps, warmup,
         if tune:
             sched = kmws.unmask_autotune(base, descs, ws, span)
         else:
-            kmws.unmask_set_schedule(ws, descs, span, schedule)
+            kmws.unmask_set_schedule(ws, schedule)
             sched = schedule
         kmws.unmask_plan(descs, ws, span)
         for _ in range(warmup):
@@ -512,7 +533,7 @@ def plain_rate(kmws, torch, dev, n, L, descs, ws, schedule, seed, steps, warmup,
             kmws.unmask_apply(base, descs, ws, span)
     kmws.unmask_batch(base, descs, ws, span)
     mism = kmws.check_unmasked(base, seed, descs)
-    kmws.unmask_set_schedule(ws, descs, span, schedule)  # the placed batch's schedule, as before
+    kmws.unmask_set_schedule(ws, schedule)  # the placed batch's schedule, as before
     del base
     torch.cuda.empty_cache()
     out["byte_mismatches"] = mism
@@ -591,12 +612,13 @@ def main():
             kmws.fill_uniform_descs(bdescs, L, L, (a.seed ^ 0x5EED) + b_lo)
             kmws.fill_synthetic(base, seed)
             if a.schedule >= 0:
-                kmws.unmask_set_schedule(ws, bdescs, bspan, a.schedule)
+                kmws.unmask_set_schedule(ws, a.schedule)
             elif j == 0 and not a.no_autotune:
                 # untimed, payload unchanged: picks this batch's faster unmask schedule
+                # (kept on ws, the host plan of the batches it serves)
                 schedule = kmws.unmask_autotune(base, bdescs, ws, bspan)
             elif not a.no_autotune:
-                kmws.unmask_set_schedule(ws, bdescs, bspan, schedule)  # same layout as batch 0
+                kmws.unmask_set_schedule(ws, schedule)  # same layout as batch 0
         torch.cuda.synchronize()
 
         def step(ev0=None, ev1=None):
@@ -669,7 +691,7 @@ def main():
     if rank == 0:
         cpu = None
         if a.cpu_seconds > 0 and world == 1:
-            thr = a.cpu_threads or host_cores()[0]
+            thr = a.cpu_threads or effective_cores()
             cpu = cpu_baseline(a.cpu_seconds, thr, L, a.seed)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,

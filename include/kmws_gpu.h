@@ -148,8 +148,9 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
  * overlaps the loop's socket reads (the EventLoop::post pattern,
  * kmapi.h:204-210).  Payload views point into the batch (or the attached
  * ring) and are valid during the callback; the caller's chunk is not
- * modified.  A callback returning nonzero ("destroyed") drops that decoder's
- * remaining frames of the generation.  Destroy a decoder only after its
+ * modified.  A callback returning nonzero ("destroyed") drops every other frame
+ * of that decoder still held by the batch: the rest of the generation, later
+ * generations in flight and the generation being fed.  Destroy a decoder only after its
  * frames were delivered or after kmws_rx_batch_discard (which also covers
  * submitted generations).  Do not mix kmws_decoder_feed and deferred feeds on
  * one decoder while its frames are pending. */
@@ -209,7 +210,8 @@ int            kmws_tx_batch_pending(const kmws_tx_batch* b);
 /* Optional pinned send ring (hipHostMalloc / hipHostRegister) the loop builds
  * its outgoing payloads in: segments inside it are masked in place there
  * (zero-copy, one launch), the others go through pinned staging.  Only while
- * no sends are queued; NULL detaches. */
+ * no sends are queued or in flight (KMWS_ERR_INVALID_STATE otherwise); NULL
+ * detaches. */
 kmws_status    kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ring_bytes);
 
 /* ======================= device batch entries ======================= */
@@ -235,7 +237,8 @@ kmws_status kmws_unmask_batch(uint8_t* base, uint64_t span, const kmws_desc* des
 
 /* kmws_unmask_batch in two stream-ordered halves: `plan` validates the
  * descriptors and builds the tile map in the workspace; `apply` runs the
- * unmask kernel.  A plan stays valid for the same (descs, n, span). */
+ * unmask kernel with the default schedule.  A plan stays valid for the same
+ * (descs, n, span). */
 kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                              size_t workspace_bytes, void* stream);
 kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
@@ -258,25 +261,34 @@ kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* des
 #define KMWS_SCHED_NT_STORES       (1 << 29)
 #define KMWS_SCHED_TEMPORAL_STORES (1 << 30)
 
+/* kmws_unmask_apply with an explicit schedule (schedule < 0: the default,
+ * kmws_unmask_default_schedule).  The library keeps no schedule state: a
+ * schedule belongs to the caller's plan of one batch (e.g. the code
+ * kmws_unmask_autotune returned for it) and is passed on every apply, like the
+ * descriptors.  An invalid code returns KMWS_ERR_INVALID_PARAM. */
+kmws_status kmws_unmask_apply_sched(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                    const void* workspace, size_t workspace_bytes, int schedule, void* stream);
+
+/* The schedule kmws_unmask_apply / kmws_unmask_batch use: split 4 from a mean
+ * frame region of 16 KiB (span / n), grouped XCD runs below; non-temporal
+ * stores. */
+int kmws_unmask_default_schedule(uint64_t span, uint32_t n);
+
 /* Optional one-time tuning of ONE batch (like a cuDNN benchmark pass): runs
  * every placement kind with both store policies twice on this batch (the XOR
  * applied twice leaves the payload unchanged), times them with events on
- * `stream` (synchronizes) and records the fastest for this batch -- the tuple
- * (workspace, descs, n, span) -- where kmws_unmask_apply / kmws_unmask_batch
- * find it.  Every other batch keeps the default schedule (split 4 or grouped
- * runs by mean region, non-temporal stores): no device-global state.  Returns the chosen schedule code
- * or a negative status. */
+ * `stream` (synchronizes) and returns the fastest schedule code (or a negative
+ * status) for the caller to pass to kmws_unmask_apply_sched.  Nothing is
+ * recorded: the next batch, on any workspace, gets the default unless its
+ * caller passes a schedule. */
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream);
-/* Pin a schedule for one batch (e.g. one measured offline), or forget it
- * (schedule < 0: back to the default).  One entry per workspace. */
-kmws_status kmws_unmask_set_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span,
-                                     int schedule);
-/* The schedule code kmws_unmask_apply uses for this batch. */
-int kmws_unmask_get_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span);
 
-/* Read (synchronously) the status word of a workspace after a batch call:
- * 0 = OK, 1 = descriptor precondition violated, 2 = header error seen. */
+/* Read (synchronously) the status word of a workspace after a batch call, a
+ * bit set: 0 = OK, 1 = descriptor precondition violated, 2 = header error seen,
+ * 4 = the header-pack scan timed out waiting for a predecessor tile's state
+ * (kmws_pack_headers: wire_off is then invalid; never seen with in-order
+ * workgroup dispatch). */
 kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream);
 
 /* ---- batched header pack / unpack (device) ---- */
@@ -313,7 +325,8 @@ size_t kmws_pack_headers_workspace_size(uint32_t n);
  * to back on the wire (exclusive scan of header + payload bytes) and the total
  * in wire_off[n]; it needs the workspace (a status word and one 8-byte scan
  * state per 2048 frames, cleared by the call; one pass over the descriptors).
- * hdr 16-B aligned. */
+ * wire_off is valid only when the workspace status (kmws_read_status) is 0
+ * afterwards.  hdr 16-B aligned. */
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,
                               uint8_t* hdr_len, uint64_t* wire_off, void* workspace, size_t workspace_bytes,
                               void* stream);

@@ -20,6 +20,7 @@ struct WsHead {
 };
 constexpr uint32_t kStatusBadDesc = 1u;
 constexpr uint32_t kStatusBadHeader = 2u;
+constexpr uint32_t kStatusLookbackTimeout = 4u;  // a scan predecessor never published: outputs invalid
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {

@@ -579,7 +579,8 @@ int kmws_tx_batch_add(kmws_tx_batch* b, const kmws_frame_hdr* hdr, uint8_t* cons
 kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ring_bytes)
 {
     if (!b || (ring && !ring_bytes)) return KMWS_ERR_INVALID_PARAM;
-    if (!b->frames.empty()) return KMWS_ERR_INVALID_STATE;  // queued segments were classified already
+    // queued segments were classified already; a mask in flight may still be writing into the old ring
+    if (!b->frames.empty() || !b->inflight.empty()) return KMWS_ERR_INVALID_STATE;
     if (ring && !device_view(ring)) return KMWS_ERR_INVALID_PARAM;  // must be pinned
     b->ring = ring;
     b->ring_bytes = ring ? ring_bytes : 0;
@@ -806,17 +807,16 @@ int kmws_rx_batch_poll(kmws_rx_batch* b, int wait)
             b->spare.push_back(std::move(stage));
             continue;
         }
-        std::vector<const kmws_decoder*> destroyed;
         b->flushing = true;
         b->delivering = &items;
         for (auto& it : items) {
             if (!it.live) continue;
-            bool dead = false;
-            for (const kmws_decoder* d : destroyed) dead |= (d == it.dec);
-            if (dead) continue;
             ++delivered;  // a NULL callback consumes the frame, like WSHandler without frame_cb_ (:286)
             uint8_t* payload = it.direct ? it.direct : stage->data() + it.off;
-            if (it.cb && it.cb(&it.hdr, payload, it.hdr.length, it.user)) destroyed.push_back(it.dec);
+            // "destroyed" (WSHandler.cpp:284-287): none of that decoder's frames
+            // may reach its callback again -- the rest of this generation, every
+            // later generation in flight and the one still being fed
+            if (it.cb && it.cb(&it.hdr, payload, it.hdr.length, it.user)) kmws_rx_batch_discard(b, it.dec);
         }
         b->delivering = nullptr;
         b->flushing = false;

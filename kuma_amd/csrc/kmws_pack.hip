@@ -1129,8 +1129,8 @@ __device__ uint64_t look_back(const uint64_t* __restrict__ st, uint32_t tile, Ws
                 if (dmin < 64) return pre;
                 break;
             }
-            if (++spins >= kLookSpinLimit) {  // cannot happen: every lower tile publishes
-                if (lane == 0) atomicOr(&head->status, kStatusBadDesc);
+            if (++spins >= kLookSpinLimit) {  // every lower tile publishes: only a stalled or broken predecessor
+                if (lane == 0) atomicOr(&head->status, kStatusLookbackTimeout);
                 return pre;
             }
             __builtin_amdgcn_s_sleep(8);
@@ -1186,7 +1186,12 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
     const bool first = tile == 0;
 #endif
     KMWS_TRACE(tile, 1);
-    if (t == 0) st_agent(st + tile, first ? agg << 2 | kStInc : agg << 2 | kStAgg);
+#ifdef KMWS_TEST_SKIP_PUBLISH_TILE  // test build only: this tile never publishes (a successor must time out)
+    const bool publish = tile != (uint32_t)(KMWS_TEST_SKIP_PUBLISH_TILE);
+#else
+    constexpr bool publish = true;
+#endif
+    if (t == 0 && publish) st_agent(st + tile, first ? agg << 2 | kStInc : agg << 2 | kStAgg);
     // then the header slots (they need no offset; stores issued ahead of the
     // publish would delay it: the vector memory queue is in order) and the sizes
     // for the per-frame scan
@@ -1226,7 +1231,7 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
         lds_barrier();
         pre = s_pre;
         KMWS_TRACE(tile, 4);
-        if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
+        if (t == 0 && publish) st_agent(st + tile, (pre + agg) << 2 | kStInc);
     }
     if (t == 0 && F + kScanTile >= n) out[n] = pre + agg;  // the last tile: the total
     uint64_t run = pre + before + inc - sum;

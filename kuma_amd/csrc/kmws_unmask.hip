@@ -14,9 +14,6 @@
 // mask (a rotated key splatted over the payload bytes of the word; header or
 // gap bytes get 0), XORs and stores whole 16-byte words.  HBM-bound: 2 bytes
 // of traffic per payload byte + 16 B per descriptor; no MFMA.
-#include <atomic>
-#include <mutex>
-
 #include "kmws_bench.h"
 #include "kmws_common.hpp"
 
@@ -531,10 +528,12 @@ static kmws_status launch_plan(uint64_t span, const kmws_desc* descs, uint32_t n
 // profiles/r01f_unmask_placement.txt, r02al_unmask_schedules_2bpc.txt) and how the
 // payload is stored (non-temporal by default; see store_word).
 //
-// A schedule belongs to ONE batch: kmws_unmask_autotune / kmws_unmask_set_schedule
-// record it for (workspace, descs, n, span), and apply uses it only for that
-// batch; every other batch gets the default, by the mean region (the same test
-// as the occupancy cap): split 4 for regions of a tile or more -- the best on
+// The library keeps no schedule state: kmws_unmask_autotune returns the code it
+// picked for the batch it timed, and the caller passes it to
+// kmws_unmask_apply_sched for that batch (the caller's plan object owns it;
+// kuma_amd/kmws.py keeps it on the Workspace).  kmws_unmask_apply and
+// kmws_unmask_batch use the default, by the mean region (the same test as the
+// occupancy cap): split 4 for regions of a tile or more -- the best on
 // plain allocations of the aligned arena (0.82), the packed wire (0.82) and
 // cfg3's Zipf wire (0.81) -- and grouped XCD runs below -- the best on 4 KiB
 // fragments (0.81 vs 0.78 for split 4)
@@ -574,56 +573,6 @@ static bool valid_schedule(uint32_t code)
 }
 
 static bool temporal_stores(uint32_t code) { return (code & kSchedTemporal) != 0; }
-
-struct TunedBatch {
-    const void* ws;
-    const void* descs;
-    uint64_t span;
-    uint32_t n;
-    uint32_t code;
-};
-constexpr int kTunedSlots = 64;
-static std::mutex g_tuned_mu;
-static TunedBatch g_tuned[kTunedSlots];
-static std::atomic<int> g_tuned_count{0};
-static int g_tuned_next = 0;
-
-static uint32_t batch_schedule(const void* ws, const kmws_desc* descs, uint32_t n, uint64_t span)
-{
-    if (g_tuned_count.load(std::memory_order_acquire) == 0) return default_schedule(span, n);
-    std::lock_guard<std::mutex> lk(g_tuned_mu);
-    for (const TunedBatch& t : g_tuned)
-        if (t.ws == ws && t.descs == descs && t.n == n && t.span == span) return t.code;
-    return default_schedule(span, n);
-}
-
-// Records (or, code < 0, forgets) the schedule of one batch.  One entry per
-// workspace: a workspace serves one batch at a time.
-static void record_schedule(const void* ws, const kmws_desc* descs, uint32_t n, uint64_t span, int64_t code)
-{
-    std::lock_guard<std::mutex> lk(g_tuned_mu);
-    int slot = -1;
-    for (int i = 0; i < kTunedSlots; ++i)
-        if (g_tuned[i].ws == ws) slot = i;
-    if (code < 0) {
-        if (slot >= 0) {
-            g_tuned[slot] = TunedBatch{};
-            g_tuned_count.fetch_sub(1, std::memory_order_release);
-        }
-        return;
-    }
-    if (slot < 0) {
-        for (int i = 0; i < kTunedSlots && slot < 0; ++i)
-            if (!g_tuned[i].ws) slot = i;
-        if (slot < 0) {  // full: the oldest slot goes (a forgotten batch reverts to the default)
-            slot = g_tuned_next;
-            g_tuned_next = (g_tuned_next + 1) % kTunedSlots;
-        } else {
-            g_tuned_count.fetch_add(1, std::memory_order_release);
-        }
-    }
-    g_tuned[slot] = TunedBatch{ws, descs, span, n, (uint32_t)code};
-}
 
 static kmws_status launch_apply(uint32_t code, uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                                 const void* workspace, size_t ws_bytes, hipStream_t s)
@@ -719,28 +668,22 @@ kmws_status kmws_unmask_plan(uint64_t span, const kmws_desc* descs, uint32_t n, 
 kmws_status kmws_unmask_apply(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
                               const void* workspace, size_t workspace_bytes, void* stream)
 {
+    return kmws_unmask_apply_sched(base, span, descs, n, workspace, workspace_bytes, -1, stream);
+}
+
+kmws_status kmws_unmask_apply_sched(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n,
+                                    const void* workspace, size_t workspace_bytes, int schedule, void* stream)
+{
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
-    return launch_apply(batch_schedule(workspace, descs, n, span), base, span, descs, n, workspace, workspace_bytes,
-                        static_cast<hipStream_t>(stream));
+    const uint32_t code = schedule < 0 ? default_schedule(span, n) : (uint32_t)schedule;
+    return launch_apply(code, base, span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
-int kmws_unmask_get_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span)
-{
-    return (int)batch_schedule(workspace, descs, n, span);
-}
-
-kmws_status kmws_unmask_set_schedule(const void* workspace, const kmws_desc* descs, uint32_t n, uint64_t span,
-                                     int schedule)
-{
-    if (!workspace) return KMWS_ERR_INVALID_PARAM;
-    if (schedule >= 0 && !valid_schedule((uint32_t)schedule)) return KMWS_ERR_INVALID_PARAM;
-    record_schedule(workspace, descs, n, span, schedule);
-    return KMWS_OK;
-}
+int kmws_unmask_default_schedule(uint64_t span, uint32_t n) { return (int)default_schedule(span, n); }
 
 // Times each schedule on the caller's batch, twice per schedule (XOR applied
-// twice is the identity, so the payload is unchanged on return), and records
-// the fastest for THIS batch (workspace, descs, n, span).  Synchronizes.
+// twice is the identity, so the payload is unchanged on return), and returns
+// the fastest; nothing is recorded.  Synchronizes.
 int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, uint32_t n, void* workspace,
                          size_t workspace_bytes, void* stream)
 {
@@ -784,7 +727,6 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (st != KMWS_OK) return st;
-    record_schedule(workspace, descs, n, span, pick);
     return (int)pick;
 }
 

@@ -31,7 +31,7 @@ EXPORTS = [
     "kmws_encode_header", "kmws_header_size", "kmws_decoder_create", "kmws_decoder_destroy",
     "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
     "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
-    "kmws_unmask_autotune", "kmws_unmask_set_schedule", "kmws_unmask_get_schedule", "kmws_read_status",
+    "kmws_unmask_autotune", "kmws_unmask_apply_sched", "kmws_unmask_default_schedule", "kmws_read_status",
     "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pack_headers_workspace_size", "kmws_pack_headers", "kmws_find_headers_streams",
@@ -53,10 +53,6 @@ BENCH_EXPORTS = [
 SCHED_GROUPED_RUNS, SCHED_IN_ORDER, SCHED_SPLIT2, SCHED_SPLIT8, SCHED_XCD_RUNS, SCHED_SPLIT4 = 0, 1, 2, 3, 4, 5
 SCHED_KINDS = (0, 1, 2, 3, 4, 5)
 
-
-def sched_default(span: int, n: int) -> int:
-    """The schedule kmws_unmask_apply uses for a batch nobody tuned."""
-    return SCHED_SPLIT4 if n and span // n >= 16384 else SCHED_GROUPED_RUNS
 SCHED_NT_STORES, SCHED_TEMPORAL_STORES = 1 << 29, 1 << 30
 
 
@@ -74,9 +70,10 @@ _lib: Optional[C.CDLL] = None
 
 
 def lib_path() -> str:
-    # KMWS_LIB: an A/B tuning build of the same ABI (tools only; the product
-    # library is kuma_amd/lib/libkmws_gpu.so)
-    return os.environ.get("KMWS_LIB") or _build.LIB
+    """The product library, always: tuning and test variants of the same ABI
+    (kuma_amd/build.py) are loaded by path by the tools and tests that need
+    them, never through this binding."""
+    return _build.LIB
 
 
 def lib() -> C.CDLL:
@@ -117,8 +114,8 @@ def lib() -> C.CDLL:
         "kmws_unmask_plan": (i32, [u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_apply": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
         "kmws_unmask_autotune": (i32, [u8p, u64, vp, u32, vp, sz, vp]),
-        "kmws_unmask_set_schedule": (i32, [vp, vp, u32, u64, i32]),
-        "kmws_unmask_get_schedule": (i32, [vp, vp, u32, u64]),
+        "kmws_unmask_apply_sched": (i32, [u8p, u64, vp, u32, vp, sz, i32, vp]),
+        "kmws_unmask_default_schedule": (i32, [u64, u32]),
         "kmws_read_status": (i32, [vp, C.POINTER(C.c_uint32), vp]),
         "kmws_fill_synthetic": (i32, [u8p, u64, u64, vp]),
         "kmws_arena_alloc": (vp, [u64, i32, C.POINTER(C.c_int)]),
@@ -174,17 +171,29 @@ class KmwsError(RuntimeError):
     def __init__(self, status: int, what: str):
         super().__init__(f"{what} failed with kmws_status {status}")
         self.status = status
+        self.ws_status = 0  # the workspace status word, when that is what failed
 
 
-def _check_tensor(t, name: str, elem: int, device) -> None:
-    """Raw data_ptr() goes to the kernels: element size, layout and device must
-    match what the C ABI reads, or it would read past the tensor."""
+def _check_tensor(t, name: str, elem: int, device, min_numel: int = 0) -> None:
+    """Raw data_ptr() goes to the kernels: element size, layout, device and
+    size must match what the C ABI reads and writes, or a kernel would access
+    memory past the tensor."""
     if t.element_size() != elem:
         raise TypeError(f"{name}: expected {elem}-byte elements, got {t.dtype}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     if t.device != device:
         raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name} has {t.numel()} elements, the call needs {min_numel}")
+
+
+def _check_descs(descs) -> int:
+    """kmws_desc array as an (n, 2) 8-byte tensor (make_descs); returns n."""
+    if descs.dim() != 2 or descs.shape[1] != 2:
+        raise ValueError(f"descs must have shape (n, 2) (kmws_desc), got {tuple(descs.shape)}")
+    _check_tensor(descs, "descs", 8, descs.device)
+    return descs.shape[0]
 
 
 def _check(st: int, what: str) -> None:
@@ -471,11 +480,18 @@ def make_descs(off, length, key, device="cuda"):
 
 
 class Workspace:
-    """Caller-owned device workspace (no allocation inside the batch calls)."""
+    """Caller-owned device workspace (no allocation inside the batch calls).
+
+    It is also the host plan of the batch it serves: `schedule` (None = the
+    library default) is the unmask schedule code its applies pass to
+    kmws_unmask_apply_sched -- set by unmask_autotune or unmask_set_schedule.
+    The library keeps no schedule state, so a new Workspace (wherever torch
+    places it) starts on the default."""
 
     def __init__(self, nbytes: int, device="cuda"):
         import torch
         self.tensor = torch.empty(max(16, int(nbytes)), dtype=torch.uint8, device=device)
+        self.schedule: Optional[int] = None
 
     @property
     def ptr(self) -> int:
@@ -534,37 +550,47 @@ def unmask_workspace_size(span: int) -> int:
     return lib().kmws_unmask_workspace_size(span)
 
 
+def _sched_arg(ws: "Workspace", schedule: Optional[int]) -> int:
+    if schedule is not None:
+        return int(schedule)
+    return -1 if ws.schedule is None else int(ws.schedule)
+
+
 def unmask_batch(base, descs, ws: Workspace, span: Optional[int] = None, stream=None,
                  schedule: Optional[int] = None) -> None:
-    """In-place batched unmask (kmws_unmask_batch) of uint8 device tensor `base`.
-    `schedule` pins a schedule code for this batch first (kmws_unmask_set_schedule)."""
+    """In-place batched unmask (kmws_unmask_plan + kmws_unmask_apply_sched) of
+    uint8 device tensor `base`, with `schedule`, else ws.schedule, else the default."""
     span = base.numel() if span is None else span
-    n = descs.shape[0]
-    if schedule is not None:
-        unmask_set_schedule(ws, descs, span, schedule)
-    _check(lib().kmws_unmask_batch(base.data_ptr(), span, descs.data_ptr(), n, ws.ptr, ws.nbytes,
-                                   _stream_handle(stream)), "kmws_unmask_batch")
+    unmask_plan(descs, ws, span, stream)
+    unmask_apply(base, descs, ws, span, stream, schedule)
 
 
 def unmask_autotune(base, descs, ws: Workspace, span: Optional[int] = None, stream=None) -> int:
-    """kmws_unmask_autotune: pick and record the schedule of THIS batch (payload unchanged)."""
+    """kmws_unmask_autotune: the fastest schedule of THIS batch (payload
+    unchanged); kept as ws.schedule, the plan of the batch ws serves."""
     span = base.numel() if span is None else span
     r = lib().kmws_unmask_autotune(base.data_ptr(), span, descs.data_ptr(), descs.shape[0], ws.ptr, ws.nbytes,
                                    _stream_handle(stream))
     if r < 0:
         raise RuntimeError(f"kmws_unmask_autotune failed with kmws_status {r}")
+    ws.schedule = r
     return r
 
 
-def unmask_set_schedule(ws: Workspace, descs, span: int, schedule: int) -> None:
-    """kmws_unmask_set_schedule: pin (schedule >= 0) or forget (< 0) this batch's schedule."""
-    _check(lib().kmws_unmask_set_schedule(ws.ptr, descs.data_ptr(), descs.shape[0], span, schedule),
-           "kmws_unmask_set_schedule")
+def unmask_set_schedule(ws: Workspace, schedule: Optional[int]) -> None:
+    """Pin (a code) or forget (None / < 0) the schedule of the batch ws serves.
+    Host-side only; an invalid code fails at the next apply."""
+    ws.schedule = None if schedule is None or schedule < 0 else int(schedule)
+
+
+def sched_default(span: int, n: int) -> int:
+    """kmws_unmask_default_schedule: the schedule of a batch nobody tuned."""
+    return lib().kmws_unmask_default_schedule(span, n)
 
 
 def unmask_get_schedule(ws: Workspace, descs, span: int) -> int:
-    """kmws_unmask_get_schedule: the schedule code apply uses for this batch."""
-    return lib().kmws_unmask_get_schedule(ws.ptr, descs.data_ptr(), descs.shape[0], span)
+    """The schedule code an apply through `ws` uses for this batch."""
+    return sched_default(span, descs.shape[0]) if ws.schedule is None else ws.schedule
 
 
 def unmask_plan(descs, ws: Workspace, span: int, stream=None) -> None:
@@ -572,10 +598,12 @@ def unmask_plan(descs, ws: Workspace, span: int, stream=None) -> None:
                                   _stream_handle(stream)), "kmws_unmask_plan")
 
 
-def unmask_apply(base, descs, ws: Workspace, span: Optional[int] = None, stream=None) -> None:
+def unmask_apply(base, descs, ws: Workspace, span: Optional[int] = None, stream=None,
+                 schedule: Optional[int] = None) -> None:
     span = base.numel() if span is None else span
-    _check(lib().kmws_unmask_apply(base.data_ptr(), span, descs.data_ptr(), descs.shape[0], ws.ptr,
-                                   ws.nbytes, _stream_handle(stream)), "kmws_unmask_apply")
+    _check(lib().kmws_unmask_apply_sched(base.data_ptr(), span, descs.data_ptr(), descs.shape[0], ws.ptr,
+                                         ws.nbytes, _sched_arg(ws, schedule), _stream_handle(stream)),
+           "kmws_unmask_apply_sched")
 
 
 def fill_synthetic(base, seed: int, nbytes: Optional[int] = None, stream=None) -> None:
@@ -606,7 +634,14 @@ def copy_workspace_size(n: int, dst_cap: int) -> int:
 
 def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None) -> None:
     """kmws_encode_batch: descs (n,2) int64, flags int16 (n,), wire_off int64 (n+1,)."""
-    _check(lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), flags.data_ptr(), descs.shape[0],
+    n = _check_descs(descs)
+    dev = descs.device
+    _check_tensor(src, "src", 1, dev)
+    _check_tensor(flags, "flags", 2, dev, n)
+    _check_tensor(dst, "dst", 1, dev)
+    _check_tensor(wire_off, "wire_off", 8, dev, n + 1)
+    _check_tensor(ws.tensor, "workspace", 1, dev)
+    _check(lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), flags.data_ptr(), n,
                                    dst.data_ptr(), dst.numel(), wire_off.data_ptr(), ws.ptr, ws.nbytes,
                                    _stream_handle(stream)), "kmws_encode_batch")
 
@@ -615,23 +650,40 @@ def pack_headers_workspace_size(n: int) -> int:
     return lib().kmws_pack_headers_workspace_size(n)
 
 
+def _capturing() -> bool:
+    import torch
+    return torch.cuda.is_current_stream_capturing()
+
+
 def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Workspace] = None,
-                 stream=None) -> None:
+                 stream=None, check: bool = True) -> None:
     """kmws_pack_headers: headers only, frame i's into the 16-B slot hdr[16 i:]
     (uint8 device tensor of >= 16 n bytes), lengths into hdr_len (uint8, n),
-    wire offsets into wire_off (int64, n+1; needs ws)."""
-    _check_tensor(descs, "descs", 8, descs.device)
-    _check_tensor(flags, "flags", 2, descs.device)
-    _check_tensor(hdr, "hdr", 1, descs.device)
+    wire offsets into wire_off (int64, n+1; needs ws).  With wire_off and
+    `check` (outside a graph capture) the workspace status is read back
+    (synchronizing) and a nonzero one -- a bad descriptor, or the look-back
+    timeout that leaves wire_off invalid -- raises KmwsError."""
+    n = _check_descs(descs)
+    dev = descs.device
+    _check_tensor(flags, "flags", 2, dev, n)
+    _check_tensor(hdr, "hdr", 1, dev, 16 * n)
     if hdr_len is not None:
-        _check_tensor(hdr_len, "hdr_len", 1, descs.device)
+        _check_tensor(hdr_len, "hdr_len", 1, dev, n)
     if wire_off is not None:
-        _check_tensor(wire_off, "wire_off", 8, descs.device)
-    _check(lib().kmws_pack_headers(descs.data_ptr(), flags.data_ptr(), descs.shape[0], hdr.data_ptr(),
+        _check_tensor(wire_off, "wire_off", 8, dev, n + 1)
+    if ws is not None:
+        _check_tensor(ws.tensor, "workspace", 1, dev)
+    _check(lib().kmws_pack_headers(descs.data_ptr(), flags.data_ptr(), n, hdr.data_ptr(),
                                    hdr_len.data_ptr() if hdr_len is not None else None,
                                    wire_off.data_ptr() if wire_off is not None else None,
                                    ws.ptr if ws is not None else None, ws.nbytes if ws is not None else 0,
                                    _stream_handle(stream)), "kmws_pack_headers")
+    if check and wire_off is not None and ws is not None and n and not _capturing():
+        st = ws.status(stream)
+        if st:
+            e = KmwsError(ERR_FAILED, f"kmws_pack_headers (workspace status {st}: wire_off invalid)")
+            e.ws_status = st
+            raise e
 
 
 def find_headers_streams(wire, stream_off, cap: int, wire_len: Optional[int] = None, stream=None):
@@ -665,7 +717,13 @@ def unpack_headers(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: W
 
 
 def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
-    _check(lib().kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), descs.shape[0], dst.data_ptr(),
+    n = _check_descs(descs)
+    dev = descs.device
+    _check_tensor(src, "src", 1, dev)
+    _check_tensor(dst, "dst", 1, dev)
+    _check_tensor(dst_off, "dst_off", 8, dev, n + 1)
+    _check_tensor(ws.tensor, "workspace", 1, dev)
+    _check(lib().kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), n, dst.data_ptr(),
                                     dst.numel(), dst_off.data_ptr(), ws.ptr, ws.nbytes,
                                     _stream_handle(stream)), "kmws_gather_unmask")
 

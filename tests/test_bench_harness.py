@@ -136,3 +136,19 @@ def test_launch_ranks_environment(tmp_path):
     assert all(x["RANK"] == x["LOCAL_RANK"] and x["WORLD_SIZE"] == "3" and x["MASTER_ADDR"] == "127.0.0.1"
                for x in rows)
     assert len({x["MASTER_PORT"] for x in rows}) == 1 and all(x["argv"] == ["--x", "1"] for x in rows)
+
+
+def test_cpu_baseline_cores_are_the_effective_count(monkeypatch):
+    """the CPU baseline runs min(affinity, ceil(cgroup quota))
+    threads and reports that number as `cores`, the 1-thread rate beside it,
+    and says the port is uncalibrated against a reference build."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for (aff, quota), want in (((256, 16.0), 16), ((256, 15.5), 16), ((8, 16.0), 8), ((64, None), 64),
+                               ((4, 0.5), 1)):
+        monkeypatch.setattr(bench, "host_cores", lambda a=aff, q=quota: (a, q))
+        assert bench.effective_cores() == want
+    monkeypatch.setattr(bench, "host_cores", lambda: (256, 2.0))
+    cb = bench.cpu_baseline(0.2, bench.effective_cores(), 4096, 1)
+    assert cb["cores"] == 2 and cb["affinity_cores"] == 256 and cb["cgroup_cpu_quota_cores"] == 2.0
+    assert cb["value"] > 0 and cb["single_core_GiB_s"] > 0 and "not calibrated" in cb["sample"]

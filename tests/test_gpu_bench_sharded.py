@@ -55,3 +55,51 @@ def test_bench_one_gpu_small_batch_plain_rate():
     assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["verify"]["byte_mismatches"] == 0
     assert d["config"]["placement"]["kind"] == "plain torch.empty"
     assert d["roofline"]["frac_plain"] == d["roofline"]["frac"] > 0  # the timed batch is the plain allocation
+
+
+CFG5_FRAMES = 10485760  # BASELINE configs[4]: 10 M x 64 KiB = 640 GiB
+CFG5_BATCH = 1310720    # bench.py --max-batch-frames default: 80 GiB resident per sub-batch
+_cfg5 = {}
+
+
+def _check_cfg5(d, world):
+    assert d["n_gpus"] == world and d["scaling"] == "strong"
+    assert d["config"]["total_frames"] == CFG5_FRAMES and d["config"]["frame_len"] == 65536
+    assert d["verify"]["byte_mismatches"] == 0 and d["verify"]["status_word"] == 0
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == list(range(world))
+    assert ranks[0]["frames"][0] == 0 and ranks[-1]["frames"][1] == CFG5_FRAMES
+    assert all(a["frames"][1] == b["frames"][0] for a, b in zip(ranks, ranks[1:]))  # contiguous shards
+    for r in ranks:
+        subs = r["sub_batches"]
+        assert len(subs) == 8 // world
+        assert subs[0][0] == r["frames"][0] and subs[-1][1] == r["frames"][1]
+        assert all(a[1] == b[0] for a, b in zip(subs, subs[1:]))
+        assert all(hi - lo == CFG5_BATCH for lo, hi in subs)
+        assert r["byte_mismatches"] == 0
+    assert d["value"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_cfg5_full_job_one_gpu():
+    """BASELINE configs[4]'s real job at N = 1 -- 10,485,760 x
+    64 KiB frames as 8 resident sub-batches of 1,310,720 frames (80 GiB), each
+    generated on the device, unmasked by the product kernels and verified byte
+    for byte."""
+    d = run_bench("--gpus", "1", "--job-frames", str(CFG5_FRAMES), "--steps", "2", "--warmup", "1",
+                  "--cpu-seconds", "0", timeout=600)
+    _check_cfg5(d, 1)
+    _cfg5[1] = d["value"]
+
+
+@pytest.mark.timeout(600)
+def test_cfg5_full_job_two_ranks_share_the_gpu():
+    """The same job at --gpus 2 (gloo harness, both ranks on the one GPU of the
+    box): 4 sub-batches per rank over contiguous shards, every byte verified;
+    the two ranks share one GPU's HBM, so the aggregate must stay within 10 %
+    of the N = 1 line (nothing is lost to the partition or the harness)."""
+    d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--job-frames", str(CFG5_FRAMES), "--steps", "2",
+                  "--warmup", "1", "--cpu-seconds", "0", timeout=600)
+    _check_cfg5(d, 2)
+    if 1 in _cfg5:
+        assert abs(d["value"] / _cfg5[1] - 1) <= 0.10, (d["value"], _cfg5[1])

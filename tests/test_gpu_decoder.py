@@ -197,6 +197,39 @@ def test_deferred_destroy_drops_only_that_connection():
     assert n == 2 + len(fb)
 
 
+def test_deferred_destroy_covers_every_generation_in_flight():
+    """a callback that reports "destroyed" must stop delivery of
+    that decoder's frames in every generation the batch still holds -- later
+    generations already submitted and the one still being fed -- while the
+    other connection's frames are all delivered."""
+    streams_a = [masked_stream(81 + g, 4, sizes=(5, 300)) for g in range(3)]
+    streams_b = [masked_stream(91 + g, 4, sizes=(7, 200)) for g in range(3)]
+    batch = kmws.RxBatch(0)
+    ha, hb = kmws.WSHandler(kmws.SERVER), kmws.WSHandler(kmws.SERVER)
+    ga, gb = [], []
+
+    def cba(hd, p):
+        ga.append(p)
+        return len(ga) == 2  # "destroyed" after its 2nd frame (generation 1)
+
+    ha.setFrameCallback(cba)
+    hb.setFrameCallback(lambda hd, p: gb.append(p))
+    for g in range(2):  # two generations submitted, in flight together
+        ha.handleDataDeferred(batch, streams_a[g])
+        hb.handleDataDeferred(batch, streams_b[g])
+        assert batch.submit() == 8
+    ha.handleDataDeferred(batch, streams_a[2])  # the generation being fed
+    hb.handleDataDeferred(batch, streams_b[2])
+    assert batch.inflight() == 2 and batch.pending() == 8
+    n = batch.poll(wait=True)
+    n += batch.flush()
+    fa = run_oracle(streams_a[0], orc.SERVER, 0)[1]
+    fb = [f[-1] for s in streams_b for f in run_oracle(s, orc.SERVER, 0)[1]]
+    assert ga == [f[-1] for f in fa[:2]]
+    assert gb == fb
+    assert n == 2 + len(fb)
+
+
 def test_mask_host_chain_golden_and_random():
     """handleDataMask(key, KMBuffer&) over host segments: phase continues across
     segments (SURVEY a-2 vector) and equals the oracle's chain mask."""

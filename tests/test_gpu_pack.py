@@ -338,6 +338,48 @@ def test_pack_headers_chain_many_tiles(T, n):
         assert np.array_equal(woff.cpu().numpy(), woff_want), rep
 
 
+def test_pack_headers_lookback_timeout_sets_its_own_bit(T):
+    """VERDICT r03 #7 / ADVICE r03: a look-back predecessor that never
+    publishes must end the wait with kStatusLookbackTimeout (4), not the
+    bad-descriptor bit, and the call must return.  Test-only library
+    (kuma_amd/build.py LOOKBACK_TEST_DEFINES): tile 1 of the header pack never
+    publishes, the spin bound is 4096 polls.  The product binding then refuses
+    the offsets (KmwsError with the workspace status)."""
+    import ctypes as C
+    from kuma_amd import build as kb
+    from kuma_amd import kmws
+    assert os.path.exists(kb.LOOKBACK_TEST_LIB), "run __graft_entry__.build()"
+    L = C.CDLL(kb.LOOKBACK_TEST_LIB)
+    vp = C.c_void_p
+    L.kmws_pack_headers.restype, L.kmws_pack_headers.argtypes = C.c_int, [vp, vp, C.c_uint32, vp, vp, vp, vp,
+                                                                         C.c_size_t, vp]
+    L.kmws_read_status.restype, L.kmws_read_status.argtypes = C.c_int, [vp, C.POINTER(C.c_uint32), vp]
+    n = 4 * 2048 + 5
+    rng = np.random.default_rng(44)
+    lens = rng.integers(0, 70000, size=n)
+    keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.int64)
+    descs = kmws.make_descs(np.zeros(n, np.int64), lens, keys)
+    fl = T.full((n,), 0x182, dtype=T.int16, device="cuda")
+    hdr = T.zeros(16 * n, dtype=T.uint8, device="cuda")
+    woff = T.zeros(n + 1, dtype=T.int64, device="cuda")
+    ws = kmws.Workspace(kmws.pack_headers_workspace_size(n))
+    h = kmws._stream_handle()
+    assert L.kmws_pack_headers(descs.data_ptr(), fl.data_ptr(), n, hdr.data_ptr(), None, woff.data_ptr(), ws.ptr,
+                               ws.nbytes, h) == 0
+    st = C.c_uint32(0)
+    assert L.kmws_read_status(ws.ptr, C.byref(st), h) == 0
+    assert st.value & 4 and not st.value & 1, st.value
+    # the product library on the same batch: clean status, offsets exact
+    kmws.pack_headers(descs, fl, hdr, None, woff, ws)
+    hl = np.where(lens <= 125, 2, np.where(lens <= 65535, 4, 10)) + 4
+    assert np.array_equal(woff.cpu().numpy(), np.concatenate([[0], np.cumsum(lens + hl)]))
+    # a nonzero status after the call surfaces as an error in the binding
+    ws.status = lambda stream=None: 4
+    with pytest.raises(kmws.KmwsError) as e:
+        kmws.pack_headers(descs, fl, hdr, None, woff, ws)
+    assert e.value.ws_status == 4
+
+
 def test_find_headers_streams_matches_host_walk(T):
     """kmws_find_headers_streams (one lane per stream) == kmws_find_headers on
     each stream: complete streams, streams cut mid-frame, a corrupted length,

@@ -217,8 +217,8 @@ def _valid_schedule(code):
 
 def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     """kmws_unmask_autotune runs every schedule twice (XOR twice = identity):
-    the payload is unchanged, the pick is recorded for THIS batch only, and
-    unmask parity holds under it."""
+    the payload is unchanged, the pick is returned (and kept on THIS
+    Workspace, the caller's plan), and unmask parity holds under it."""
     torch = torch_dev
     from kuma_amd import kmws
     rng = np.random.default_rng(31)
@@ -230,23 +230,32 @@ def test_autotune_keeps_payload_and_picks_valid_schedule(torch_dev):
     assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == choice
     ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
     dflt = kmws.sched_default(len(buf), len(descs))
-    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == dflt  # other batches: default
-    assert kmws.unmask_get_schedule(ws, d_desc, len(buf) - 16) == kmws.sched_default(len(buf) - 16, len(descs))
+    assert kmws.unmask_get_schedule(ws2, d_desc, len(buf)) == dflt  # other plans: default
     assert np.array_equal(d_buf.cpu().numpy()[:len(buf)], buf)
     want = buf.copy()
     orc.unmask_batch(want, descs)
     kmws.unmask_batch(d_buf, d_desc, ws, len(buf))
     torch.cuda.synchronize()
     assert ws.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
-    kmws.unmask_set_schedule(ws, d_desc, len(buf), -1)  # forget: back to the default
+    kmws.unmask_set_schedule(ws, None)  # forget: back to the default
     assert kmws.unmask_get_schedule(ws, d_desc, len(buf)) == dflt
 
 
-def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
-    """ADVICE r02 / VERDICT r02 #4: tuning an aligned arena (which may pick
-    temporal stores) must not change how a packed wire image is unmasked later
-    in the same process: the wire keeps the default schedule (non-temporal
-    stores), and both batches stay bit-exact."""
+def test_default_schedule_matches_rule(torch_dev):
+    from kuma_amd import kmws
+    assert kmws.sched_default(1 << 30, 1 << 14) == kmws.SCHED_SPLIT4       # 64 KiB regions
+    assert kmws.sched_default(1 << 30, 1 << 16) == kmws.SCHED_SPLIT4       # exactly one tile
+    assert kmws.sched_default(1 << 30, (1 << 16) + 1) == kmws.SCHED_GROUPED_RUNS
+    assert kmws.sched_default(1 << 20, 0) == kmws.SCHED_GROUPED_RUNS
+
+
+def test_tuned_workspace_freed_new_one_at_same_address_gets_default(torch_dev):
+    """the library holds no pointer-keyed schedule table.  A
+    tuned Workspace is freed; torch's caching allocator hands its block to a
+    new Workspace serving another batch at the same descriptor address; that
+    batch runs the default schedule, and both stay bit-exact.  The C entries
+    take the schedule as an argument: a plain kmws_unmask_apply on the old
+    pointers after the tune is the default schedule too."""
     torch = torch_dev
     from kuma_amd import kmws
     n, L = 4096, 65536
@@ -256,32 +265,54 @@ def test_tuned_aligned_batch_leaves_packed_wire_on_default(torch_dev):
     kmws.fill_synthetic(base, 5)
     kmws.fill_uniform_descs(descs, L, L, 6)
     ws = kmws.Workspace(kmws.unmask_workspace_size(span))
-    kmws.unmask_set_schedule(ws, descs, span, kmws.SCHED_SPLIT2 | kmws.SCHED_TEMPORAL_STORES)  # as a tune may pick
-    assert kmws.unmask_get_schedule(ws, descs, span) == kmws.SCHED_SPLIT2 | kmws.SCHED_TEMPORAL_STORES
+    kmws.unmask_set_schedule(ws, kmws.SCHED_SPLIT2 | kmws.SCHED_TEMPORAL_STORES)  # as a tune may pick
     picked = kmws.unmask_autotune(base, descs, ws, span)
-    assert kmws.unmask_get_schedule(ws, descs, span) == picked
-    rng = np.random.default_rng(77)
-    buf, wd = layout("packed_wire", rng)
-    d_buf, d_desc = _to_dev(torch, buf, wd)
-    ws2 = kmws.Workspace(kmws.unmask_workspace_size(len(buf)))
-    got = kmws.unmask_get_schedule(ws2, d_desc, len(buf))
-    assert got == kmws.sched_default(len(buf), len(wd)) and not got & kmws.SCHED_TEMPORAL_STORES
-    want = buf.copy()
-    orc.unmask_batch(want, wd)
-    kmws.unmask_batch(d_buf, d_desc, ws2, len(buf))
-    torch.cuda.synchronize()
-    assert ws2.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
+    assert ws.schedule == picked
     kmws.unmask_batch(base, descs, ws, span)  # the aligned batch under its tuned schedule
     assert ws.status() == 0 and kmws.check_unmasked(base, 5, descs) == 0
+    old_ws, old_desc = ws.ptr, descs.data_ptr()
+    ws_bytes = ws.nbytes
+    del ws
+    torch.cuda.synchronize()
+    ws2 = kmws.Workspace(ws_bytes)
+    assert ws2.ptr == old_ws  # torch recycled the block
+    # another batch through it: a packed wire image
+    rng = np.random.default_rng(77)
+    buf, wd = layout("packed_wire", rng)
+    d_buf, _ = _to_dev(torch, buf, wd)
+    assert ws2.schedule is None
+    got = kmws.unmask_get_schedule(ws2, descs, len(buf))
+    assert got == kmws.sched_default(len(buf), n) and not got & kmws.SCHED_TEMPORAL_STORES
+    wdesc = torch.from_numpy(wd.view(np.int64).reshape(-1, 2).copy()).cuda()
+    want = buf.copy()
+    orc.unmask_batch(want, wd)
+    kmws.unmask_batch(d_buf, wdesc, ws2, len(buf))
+    torch.cuda.synchronize()
+    assert ws2.status() == 0 and np.array_equal(d_buf.cpu().numpy()[:len(buf)], want)
+    # the raw C apply on the tuned batch's own pointers: default schedule, still exact
+    kmws.fill_synthetic(base, 9)
+    lib = kmws.lib()
+    assert lib.kmws_unmask_plan(span, old_desc, n, ws2.ptr, ws2.nbytes, kmws._stream_handle()) == 0
+    assert lib.kmws_unmask_apply(base.data_ptr(), span, old_desc, n, ws2.ptr, ws2.nbytes,
+                                 kmws._stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert ws2.status() == 0 and kmws.check_unmasked(base, 9, descs) == 0
 
 
-def test_set_schedule_rejects_bad_codes(torch_dev):
+def test_apply_sched_rejects_bad_codes(torch_dev):
     from kuma_amd import kmws
     ws = kmws.Workspace(1024)
     d = torch_dev.zeros((1, 2), dtype=torch_dev.int64, device="cuda")
+    b = torch_dev.zeros(64, dtype=torch_dev.uint8, device="cuda")
+    h = kmws._stream_handle()
     for bad in (6, 64, 0xFF, (1 << 29) | (1 << 30), 1 << 28, 65537):
-        assert kmws.lib().kmws_unmask_set_schedule(ws.ptr, d.data_ptr(), 1, 64, bad) == kmws.ERR_INVALID_PARAM
-    assert kmws.lib().kmws_unmask_set_schedule(None, d.data_ptr(), 1, 64, 0) == kmws.ERR_INVALID_PARAM
+        assert kmws.lib().kmws_unmask_apply_sched(b.data_ptr(), 64, d.data_ptr(), 1, ws.ptr, ws.nbytes, bad,
+                                                  h) == kmws.ERR_INVALID_PARAM
+    assert kmws.lib().kmws_unmask_apply_sched(b.data_ptr(), 64, d.data_ptr(), 1, None, 0, 0, h) == \
+        kmws.ERR_INVALID_PARAM
+    ws.schedule = 6  # an invalid pinned code fails at the apply, loudly
+    with pytest.raises(RuntimeError):
+        kmws.unmask_apply(b, d, ws, 64)
 
 
 @pytest.mark.parametrize("frame_len,tail", [(65536, 0), (65531, 0), (3000, 0), (65531, 7 * 16384 + 100)])
