@@ -311,14 +311,17 @@ def run_cfg1(reps: int = 10) -> dict:
                                       "WSHandler::handleData (state machine + byte loop), SERVER mode"}}
     if kmws.device_count() > 0:
         K = kmws.lib()
-        t_gpu = run(lambda: K.kmws_decoder_create(1, 0),
-                    lambda d, b, l: K.kmws_decoder_feed(d, b, l, C.cast(None, kmws.FRAME_CB), None),
-                    K.kmws_decoder_destroy)
-        res["product_decoder_sync"] = {"GiB_s": n * L / t_gpu / 2**30, "us_per_frame": t_gpu / n * 1e6,
-                                       "best_of": reps,
-                                       "note": "kmws_decoder_feed: host parse + one GPU unmask per 64 KiB read "
-                                               "(pageable chunk -> pinned staging, zero-copy kernel); bounded "
-                                               "below by one HIP launch + stream sync per read"}
+        for key, resident in (("product_decoder_sync", True), ("product_decoder_sync_launch", False)):
+            kmws.resident_enable(resident)
+            t_gpu = run(lambda: K.kmws_decoder_create(1, 0),
+                        lambda d, b, l: K.kmws_decoder_feed(d, b, l, C.cast(None, kmws.FRAME_CB), None),
+                        K.kmws_decoder_destroy)
+            res[key] = {"GiB_s": n * L / t_gpu / 2**30, "us_per_frame": t_gpu / n * 1e6, "best_of": reps,
+                        "note": "kmws_decoder_feed: host parse + one GPU unmask per 64 KiB read (pageable chunk -> "
+                                "pinned staging, zero-copy over PCIe) " +
+                                ("by the thread's resident worker (no launch per read)" if resident else
+                                 "with the resident worker off: one HIP launch + event wait per read")}
+        kmws.resident_enable(True)
         # deferred: every read of the burst fed, ONE flush (one GPU batch per loop iteration)
         nullcb = C.cast(None, kmws.FRAME_CB)
         bufs = [bytes(wire[i:i + chunk]) for i in range(0, len(wire), chunk)]

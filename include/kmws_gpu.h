@@ -346,10 +346,34 @@ kmws_status kmws_unpack_headers(const uint8_t* wire, uint64_t wire_len, const ui
                                 int mode, kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err,
                                 void* workspace, size_t workspace_bytes, void* stream);
 
+/* kmws_unpack_headers and kmws_unmask_batch fused: the descriptor-indexed
+ * decode in place, as kuma unmasks in the caller's buffer (WSHandler.cpp:
+ * 247-260).  One kernel parses every header (the kmws_unpack_headers rules and
+ * outputs) and writes the unmask plan -- frame i's region is [hdr_off[i],
+ * hdr_off[i+1]) -- then the unmask kernel runs on the wire in place with
+ * `schedule` (< 0: the default).  workspace: kmws_unmask_workspace_size(wire_len);
+ * wire 16-byte aligned.  A header error sets out_err and status bit 2 and
+ * leaves that frame masked (len 0), the others are unmasked; offsets out of
+ * order or past wire_len set status bit 1 and nothing is unmasked. */
+kmws_status kmws_unpack_unmask(uint8_t* wire, uint64_t wire_len, const uint64_t* hdr_off, uint32_t n, int mode,
+                               kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err, void* workspace,
+                               size_t workspace_bytes, int schedule, void* stream);
+
 /* Out-of-place unmask: frame i's payload src[descs[i].off .. +len) XOR its key
  * is written densely to dst at dst_off[i] (exclusive scan of len; n+1
  * entries, dst_off[n] = total).  Nothing is written if total > dst_cap. */
 kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint32_t n, uint8_t* dst,
+                               uint64_t dst_cap, uint64_t* dst_off, void* workspace, size_t workspace_bytes,
+                               void* stream);
+
+/* kmws_unpack_headers and kmws_gather_unmask fused: the header parse runs
+ * inside the gather's first (scan) kernel, which writes out_desc / out_flags /
+ * out_err exactly as kmws_unpack_headers does; the payloads are then gathered
+ * densely into dst as kmws_gather_unmask does (error frames: len 0).
+ * workspace: kmws_copy_workspace_size(n, dst_cap); wire and dst 16-byte
+ * aligned.  Status bit 2: a header error was seen. */
+kmws_status kmws_unpack_gather(const uint8_t* wire, uint64_t wire_len, const uint64_t* hdr_off, uint32_t n, int mode,
+                               kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err, uint8_t* dst,
                                uint64_t dst_cap, uint64_t* dst_off, void* workspace, size_t workspace_bytes,
                                void* stream);
 

@@ -97,4 +97,17 @@ inline uint64_t piece_count(uint64_t off, uint32_t len)
 kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,
                                  hipStream_t s);
 
+// Resident worker (kmws_resident.hip): synchronous host jobs of at most
+// kResMaxDescs payloads and kResMaxBytes bytes go to a workgroup that stays on
+// the GPU polling pinned memory, instead of a launch + wait per call.
+constexpr int kResMaxDescs = 128;
+constexpr uint64_t kResMaxBytes = 1u << 20;
+// Unmasks descs[0..n) over dev_base and descs2[0..n2) over dev_base2 (device
+// views of pinned host memory, offsets relative to them), synchronously.
+// KMWS_ERR_NOT_SUPPORTED: too large for one job, or no worker on this thread
+// and device -- the caller launches instead.  Any other error: the job may or
+// may not have run.
+kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
+                            const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2);
+
 }  // namespace kmws

@@ -126,9 +126,23 @@ public:
     // buffer of extra_span bytes, if given), then wait for the GPU.  One launch
     // per buffer (launch_unmask_pieces) reading descriptors and piece list from
     // pinned memory: no plan kernels, no copies, no status read-back.
+    // Small jobs go to this thread's resident worker (no launch, no event wait;
+    // kmws_resident.hip); larger ones are launched on the stage's stream.
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                     const std::vector<kmws_desc>* extra = nullptr)
     {
+        const size_t n2 = extra ? extra->size() : 0;
+        if (descs_.size() + n2 <= (size_t)kResMaxDescs && descs_.size() + n2 > 0) {
+            bool ok = true;
+            for (size_t i = 0; i < n2; ++i) ok &= (*extra)[i].off + (*extra)[i].len <= extra_span;
+            if (!ok) return KMWS_ERR_INVALID_PARAM;
+            const uint8_t* dv2 = n2 ? static_cast<const uint8_t*>(device_view(extra_base)) : nullptr;
+            if (n2 && !dv2) return KMWS_ERR_INVALID_PARAM;
+            if (descs_.size() && !dv_h_) return KMWS_ERR_FAILED;
+            const kmws_status st = resident_unmask(device_, descs_.data(), dv_h_, descs_.size(),
+                                                   n2 ? extra->data() : nullptr, dv2, n2);
+            if (st != KMWS_ERR_NOT_SUPPORTED) return st;
+        }
         kmws_status st = launch(extra_base, extra_span, extra);
         if (st != KMWS_OK) return st;
         return wait();

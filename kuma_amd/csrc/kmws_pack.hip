@@ -26,16 +26,12 @@
 // device (kmws_find_headers_streams): the serial header-chain walk, one lane
 // per stream.
 #include "kmws_common.hpp"
+#include "kmws_frame_parse.hpp"
 
 namespace kmws {
 
 constexpr int kScanItems = 8;                      // frames per lane in reduce_kernel
 constexpr int kScanTile = kBlock * kScanItems;     // 2048 frames per block
-
-__host__ __device__ __forceinline__ uint32_t hdr_len(uint32_t len, uint32_t mask)
-{
-    return (len <= 125 ? 2u : (len <= 0xFFFFu ? 4u : 10u)) + (mask ? 4u : 0u);
-}
 
 // Header bytes of WSHandler::encodeFrameHeader as two little-endian u64
 // (byte k of the header = byte k of h[k >> 3]).
@@ -120,6 +116,7 @@ struct SizeRaw {
 };
 struct WireSize {
     static constexpr bool kHeaders = true;
+    static constexpr bool kClearsStatus = true;  // reduce_kernel clears the status word
     const kmws_desc* d;
     const uint16_t* flags;
     __device__ SizeRaw load(uint32_t f) const { return SizeRaw{d[f].len, flags[f]}; }
@@ -131,8 +128,34 @@ struct WireSize {
 };
 struct PayloadSize {
     static constexpr bool kHeaders = false;
+    static constexpr bool kClearsStatus = true;
     const kmws_desc* d;
     __device__ SizeRaw load(uint32_t f) const { return SizeRaw{d[f].len, 0u}; }
+    __device__ V2 value(SizeRaw x) const { return V2{x.len, unit_bound(x.len)}; }
+};
+// The descriptor-indexed decode fused into the gather's scan
+// (kmws_unpack_gather): load() parses frame f's header where it lies in the
+// wire (unpack_one: the frame's descriptor, flags and WSError are written for
+// the prologue and copy kernels that follow) and yields its payload length.
+// A header error ORs the status word during the kernel, so the word is
+// cleared by a launch before it, not by reduce_kernel.
+struct HeaderPayloadSize {
+    static constexpr bool kHeaders = false;
+    static constexpr bool kClearsStatus = false;
+    const uint8_t* wire;
+    uint64_t wire_len;
+    const uint64_t* hdr_off;
+    uint32_t n;
+    int mode;
+    kmws_desc* out_desc;
+    uint16_t* out_flags;
+    uint8_t* out_err;
+    WsHead* head;
+    __device__ SizeRaw load(uint32_t f) const
+    {
+        const kmws_desc o = unpack_one(wire, wire_len, hdr_off, n, f, mode, out_desc, out_flags, out_err, head);
+        return SizeRaw{o.len, 0u};
+    }
     __device__ V2 value(SizeRaw x) const { return V2{x.len, unit_bound(x.len)}; }
 };
 
@@ -200,7 +223,8 @@ __global__ void __launch_bounds__(kBlock) reduce_kernel(Size size, uint32_t n, V
     __shared__ V2 s_row[kRowsPerTile];
     const uint32_t t = threadIdx.x;
     // the batch's status word starts clear (set only by the kernels after this one)
-    if (blockIdx.x == 0 && t == 0) head->status = 0;
+    if constexpr (Size::kClearsStatus)
+        if (blockIdx.x == 0 && t == 0) head->status = 0;
     const uint64_t F = (uint64_t)blockIdx.x * kScanTile;
     SizeRaw raw[kRowsPerTile];
 #pragma unroll
@@ -269,42 +293,6 @@ __global__ void __launch_bounds__(kBlock) scan_tiles_kernel(V2* __restrict__ til
         tiles[ntiles] = carry;
         out_a[n] = carry.a;
     }
-}
-
-// Dword I of the 8-dword window lo||hi (I fixed at compile time).
-template <int I>
-__device__ __forceinline__ uint32_t dw(const u32x4& lo, const u32x4& hi)
-{
-    if constexpr (I == 0) return lo.x;
-    else if constexpr (I == 1) return lo.y;
-    else if constexpr (I == 2) return lo.z;
-    else if constexpr (I == 3) return lo.w;
-    else if constexpr (I == 4) return hi.x;
-    else if constexpr (I == 5) return hi.y;
-    else if constexpr (I == 6) return hi.z;
-    else return hi.w;
-}
-
-// Dword q + K of the window for q in 0..3 (per lane): a select chain over
-// distinct registers (an indexed register array would be placed in scratch).
-template <int K>
-__device__ __forceinline__ uint32_t pick(const u32x4& lo, const u32x4& hi, uint32_t q)
-{
-    const uint32_t a = (q & 1u) ? dw<K + 1>(lo, hi) : dw<K>(lo, hi);
-    const uint32_t b = (q & 1u) ? dw<K + 3>(lo, hi) : dw<K + 2>(lo, hi);
-    return (q & 2u) ? b : a;
-}
-
-// 16 bytes starting at byte delta (0..15) of the 32-byte window lo||hi.
-__device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t delta)
-{
-    const uint32_t q = delta >> 2;
-    const uint32_t r = (delta & 3u) * 8u;
-    const uint32_t c0 = pick<0>(lo, hi, q), c1 = pick<1>(lo, hi, q), c2 = pick<2>(lo, hi, q),
-                   c3 = pick<3>(lo, hi, q), c4 = pick<4>(lo, hi, q);
-    // v_alignbit_b32(hi, lo, 0) == lo, so r == 0 needs no special case
-    return u32x4{__builtin_amdgcn_alignbit(c1, c0, r), __builtin_amdgcn_alignbit(c2, c1, r),
-                 __builtin_amdgcn_alignbit(c3, c2, r), __builtin_amdgcn_alignbit(c4, c3, r)};
 }
 
 // W[k] = h[k - s] (0 where k - s is outside 0..15), s in [-15, 15].
@@ -900,31 +888,8 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
 }
 
 // ------------------------------ header unpack / validate ------------------------------
-// Byte k (0..15) of a 16-byte register word.
-__device__ __forceinline__ uint32_t byte_of(const u32x4& v, uint32_t k)
-{
-    const uint32_t q = k >> 2;
-    const uint32_t w = (q & 2u) ? ((q & 1u) ? v.w : v.z) : ((q & 1u) ? v.y : v.x);
-    return (w >> (8u * (k & 3u))) & 0xFFu;
-}
-
-// The 127-class extended length as the reference computes it on x86-64
-// (WSHandler.cpp:176-197): xpl64 |= data[pos] << ((8-k-1) << 3) with a 32-bit
-// int operand, so byte k (0..7) contributes (u64)(i64)(i32)(b << ((7-k)*8 & 31))
-// -- bytes 0..3 alias onto bits 24/16/8/0, bytes 0 and 4 sign-extend.
-// hw holds the header from byte 0; the length bytes are 2..9.
-__device__ __forceinline__ uint64_t ext_len127(const u32x4& hw)
-{
-    uint64_t x = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) x |= (uint64_t)(int64_t)(int32_t)(byte_of(hw, 2 + k) << (((7u - k) * 8u) & 31u));
-    return x;
-}
-
-// One lane per frame: the reference's HDR1..MASKEY rules (WSHandler.cpp:118-234).
-// The (at most 14) header bytes come from ONE pair of aligned 16-byte loads,
-// funnel-shifted into a register word, when both words lie inside the wire;
-// headers within 32 bytes of its end are read byte by byte (same rules).
+// One lane per frame: the reference's HDR1..MASKEY rules (parse_frame_header,
+// kmws_frame_parse.hpp).
 __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* __restrict__ wire, uint64_t wire_len,
                                                                 const uint64_t* __restrict__ hdr_off, uint32_t n,
                                                                 int mode, kmws_desc* __restrict__ out_desc,
@@ -934,92 +899,7 @@ __global__ void __launch_bounds__(kBlock) unpack_headers_kernel(const uint8_t* _
 {
     const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
     if (f >= n) return;
-    const uint64_t h = hdr_off[f];
-    const uint64_t limit = f + 1 < n ? hdr_off[f + 1] : wire_len;  // this frame must end by the next header
-    // the header window: bytes h .. h + 15 that lie inside the wire (avail of them)
-    const uint64_t avail = h < wire_len ? (wire_len - h < 16 ? wire_len - h : 16) : 0;
-    u32x4 hw = u32x4{0, 0, 0, 0};
-    // aligned 16-byte words by absolute address: a word holding any wire byte is
-    // readable (it cannot cross a page), whatever the wire's own alignment
-    const uintptr_t a = reinterpret_cast<uintptr_t>(wire + h);
-    const uintptr_t a16 = a & ~(uintptr_t)15;
-    const uintptr_t end16 = (reinterpret_cast<uintptr_t>(wire) + wire_len + 15) & ~(uintptr_t)15;
-    if (h < wire_len && a16 + 32 <= end16) {
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(a16);
-        const u32x4 hi = *reinterpret_cast<const u32x4*>(a16 + 16);
-        hw = funnel16(lo, hi, (uint32_t)(a & 15u));
-    } else {
-        for (uint32_t k = 0; k < (uint32_t)avail; ++k) {
-            const uint32_t b = wire[h + k];
-            const uint32_t sh = 8u * (k & 3u);
-            if ((k >> 2) == 0) hw.x |= b << sh;
-            else if ((k >> 2) == 1) hw.y |= b << sh;
-            else if ((k >> 2) == 2) hw.z |= b << sh;
-            else hw.w |= b << sh;
-        }
-    }
-    uint8_t err = KMWS_WS_NOERR;
-    uint32_t len = 0, key = 0, hl = 2;
-    uint32_t b0 = 0, b1 = 0;
-    if (h + 2 > wire_len || limit < h || limit > wire_len) {
-        err = h + 2 > wire_len ? KMWS_WS_NEED_MORE_DATA : KMWS_WS_INVALID_FRAME;
-    } else {
-        b0 = hw.x & 0xFFu;
-        b1 = (hw.x >> 8) & 0xFFu;
-        const uint32_t fin = b0 >> 7, op = b0 & 0x0F, mask = b1 >> 7, plen = b1 & 0x7F;
-        if (!fin && op >= 8) {
-            err = KMWS_WS_PROTOCOL_ERROR;                     // :126-130
-        } else if (op >= 8 && plen > 125) {
-            err = KMWS_WS_PROTOCOL_ERROR;                     // :145-149
-        } else {
-            const uint32_t ext = plen == 126 ? 2u : (plen == 127 ? 8u : 0u);
-            hl = 2 + ext + (mask ? 4u : 0u);
-            if (h + 2 + ext > wire_len) {
-                err = KMWS_WS_NEED_MORE_DATA;
-            } else if (plen == 126) {                          // :159-175
-                len = (byte_of(hw, 2) << 8) | byte_of(hw, 3);
-                if (len < 126) err = KMWS_WS_INVALID_LENGTH;
-            } else if (plen == 127) {                          // :176-197, x86-64 shift quirk
-                const uint64_t x = ext_len127(hw);
-                if ((x >> 63) != 0) err = KMWS_WS_INVALID_LENGTH;
-                else {
-                    len = (uint32_t)x;
-                    if (len > KMWS_MAX_FRAME_DATA_LENGTH) err = KMWS_WS_INVALID_LENGTH;
-                }
-            } else {
-                len = plen;
-            }
-            if (err == KMWS_WS_NOERR) {
-                if (mask && mode == KMWS_MODE_CLIENT) err = KMWS_WS_PROTOCOL_ERROR;          // :208-212
-                else if (!mask && mode == KMWS_MODE_SERVER && len > 0) err = KMWS_WS_PROTOCOL_ERROR;  // :225-229
-                else if (h + hl > wire_len) err = KMWS_WS_NEED_MORE_DATA;
-                else if (mask) {  // key bytes verbatim at hl - 4 (2, 4 or 10)
-                    const uint32_t k0 = hl - 4;
-                    key = byte_of(hw, k0) | (byte_of(hw, k0 + 1) << 8) | (byte_of(hw, k0 + 2) << 16) |
-                          (byte_of(hw, k0 + 3) << 24);
-                }
-                if (err == KMWS_WS_NOERR) {
-                    if (h + hl + len > wire_len) err = KMWS_WS_NEED_MORE_DATA;
-                    else if (h + hl + len > limit) err = KMWS_WS_INVALID_FRAME;  // offsets disagree with the stream
-                }
-            }
-            if (err == KMWS_WS_NOERR && !mask) key = 0;
-        }
-    }
-    kmws_desc o;
-    if (err == KMWS_WS_NOERR) {
-        o.off = h + hl;
-        o.len = len;
-        o.key = key;
-    } else {  // error frames carry no payload (nothing downstream touches them)
-        o.off = h;
-        o.len = 0;
-        o.key = 0;
-        atomicOr(&head->status, kStatusBadHeader);
-    }
-    out_desc[f] = o;
-    if (out_flags) out_flags[f] = (uint16_t)((b0 & 0xFFu) | ((b1 >> 7) << 8));
-    if (out_err) out_err[f] = err;
+    unpack_one(wire, wire_len, hdr_off, n, f, mode, out_desc, out_flags, out_err, head);
 }
 
 // ------------------------------ header pack only ------------------------------
@@ -1071,10 +951,17 @@ __global__ void __launch_bounds__(kBlock) pack_headers_kernel(const kmws_desc* _
 // inclusive prefix), written and read with agent-scope atomics (the XCDs' L2s
 // are not coherent for plain accesses); zeroed by a kernel before each call.  A
 // block waits only on lower-indexed blocks, which the dispatcher placed before
-// it; the spin is bounded all the same (a state that never arrives sets the
-// status instead of hanging).
+// it, so the wait always ends; the spin is bounded all
+// the same, far beyond any real wait (2^24 polls of >= 8 x 64 cycles plus a
+// load: seconds), and a state that never arrives sets kStatusLookbackTimeout --
+// its own status bit, not the bad-input one -- instead of hanging; wire_off is
+// then invalid.  A test build lowers the bound and skips one tile's publish
+// (KMWS_TEST_SKIP_PUBLISH_TILE, tests/test_gpu_pack.py).
 constexpr uint64_t kStAgg = 1ull, kStInc = 2ull;
-constexpr uint32_t kLookSpinLimit = 1u << 20;
+#ifndef KMWS_LOOKBACK_SPIN_LIMIT
+#define KMWS_LOOKBACK_SPIN_LIMIT (1u << 24)
+#endif
+constexpr uint32_t kLookSpinLimit = KMWS_LOOKBACK_SPIN_LIMIT;
 
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
 {
@@ -1410,6 +1297,10 @@ static kmws_status launch_reduce(Size size, uint32_t n, uint64_t* out, CopyWs& c
 // prologue (offsets, edge words, unit records), the copy grid.  Four launches,
 // stream-ordered, nothing on the host in between.
 template <bool HEADERS>
+static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                    const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s);
+
+template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
                                const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
@@ -1420,6 +1311,14 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
     const kmws_status st = HEADERS ? launch_reduce(WireSize{d, flags}, n, start, c, s)
                                    : launch_reduce(PayloadSize{d}, n, start, c, s);
     if (st != KMWS_OK) return st;
+    return launch_copy_tail<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
+}
+
+// The prologue and the copy grid, after the scan.
+template <bool HEADERS>
+static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                    const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
+{
     const uint32_t nt = (uint32_t)n_tiles(n);
     hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
                        c.head, c.tiles, nt, c.grp, start, c.rec, c.edge);
@@ -1471,6 +1370,30 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
+}
+
+// Header parse fused into the gather: status cleared, reduce over the parsed
+// payload lengths (writing the descriptors), scan, prologue, copy -- the
+// kmws_unpack_headers launch and its status clear are gone.
+kmws_status kmws_unpack_gather(const uint8_t* wire, uint64_t wire_len, const uint64_t* hdr_off, uint32_t n, int mode,
+                               kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err, uint8_t* dst,
+                               uint64_t dst_cap, uint64_t* dst_off, void* workspace, size_t workspace_bytes,
+                               void* stream)
+{
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    CopyWs c;
+    if (!dst_off || (n && (!wire || !hdr_off || !out_desc || !dst)) || (reinterpret_cast<uintptr_t>(dst) & 15u) ||
+        (reinterpret_cast<uintptr_t>(wire) & 15u) || (mode != KMWS_MODE_CLIENT && mode != KMWS_MODE_SERVER) ||
+        !carve(workspace, workspace_bytes, n, dst_cap, c))
+        return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
+                                                                       : KMWS_ERR_INVALID_PARAM;
+    if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+    if (n == 0) return launch_zero(dst_off, sizeof(uint64_t), s);
+    kmws_status st = launch_reduce(HeaderPayloadSize{wire, wire_len, hdr_off, n, mode, out_desc, out_flags, out_err,
+                                                     c.head},
+                                   n, dst_off, c, s);
+    if (st != KMWS_OK) return st;
+    return launch_copy_tail<false>(wire, dst, dst_cap, dst_off, out_desc, nullptr, n, c, s);
 }
 
 // head, then one 64-bit state per 2048-frame tile (pack_headers_chain_kernel)

@@ -1,0 +1,393 @@
+// Resident unmask worker: the synchronous host entries without a kernel launch
+// per call.
+//
+// kuma calls WSHandler::handleData once per <= 64 KiB socket read
+// (TcpConnection.cpp:229-233 -> WebSocketImpl.cpp:225-246) and
+// WSHandler::handleDataMask once per send (WebSocketImpl.cpp:388, :414), and
+// expects the payload unmasked when the call returns.  A stream launch plus an
+// event wait costs 13-15 us per call -- about what kuma's byte loop
+// (WSHandler.cpp:303-310) spends on a whole 64 KiB read -- so the synchronous
+// drop-in lost to the reference.  Here one workgroup of 1024
+// lanes stays resident on the GPU per host thread and device and polls a
+// mailbox in pinned host memory: the host writes a job (up to kResMaxDescs
+// payloads, each a device-visible address, a length and a key) and bumps the
+// job number; the worker sees it over PCIe, unmasks every payload in place
+// there (zero-copy, 4 x 16-byte words per lane in flight: 64 KiB per round),
+// makes its stores visible system-wide and writes the job number back; the
+// host spins on that word.  No launch, no completion signal, no interrupt.
+//
+// The worker exits by itself after kResIdleMs (5 ms) without a job (and on quit):
+// every wave reaches the exit, the grid drains, and a host thread that stops
+// feeding never leaves a kernel behind.  The next job relaunches it.  It runs
+// on a stream of its own created with a CU mask, which gets a hardware queue
+// of its own, so work on other streams never queues behind it.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "kmws_bench.h"
+#include "kmws_host_util.hpp"
+
+namespace kmws {
+
+constexpr int kResBlock = 1024;  // 16 waves: 4 words each = 64 KiB of loads in flight
+constexpr int kResWords = 4;
+// Idle exit: short, because hipDeviceSynchronize (torch.cuda.synchronize) waits
+// for every stream of the device, this kernel's included (measured: a device
+// synchronize issued while a 50 ms-idle worker sat waiting took 50 ms); a loop
+// thread under load feeds far more often than this, and a worker that idled
+// out costs one launch, the price of every call without it.
+constexpr uint32_t kResIdleMs = 5;
+
+static inline void cpu_relax()
+{
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+    __builtin_ia32_pause();
+#endif
+}
+
+struct ResDesc {  // one payload: device-visible address, bytes, LE key of its first byte
+    uint64_t addr;
+    uint32_t len;
+    uint32_t key;
+};
+static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
+
+// Pinned host memory, polled by the worker.  Host-written and device-written
+// words sit in different 128-byte lines.
+struct alignas(256) ResMailbox {
+    uint64_t seq;   // job number, written last by the host (release)
+    uint64_t quit;  // nonzero: exit at the next poll
+    uint32_t ndesc;
+    uint32_t pad0;
+    uint64_t pad1[5];
+    ResDesc desc[kResMaxDescs];
+    alignas(128) uint64_t done;    // job number finished (device, release: payloads visible)
+    alignas(128) uint64_t exited;  // incarnation number of the worker that exited
+    alignas(128) uint64_t pad2[16];
+};
+
+// Loads of host-written words bypass every cache (and are never scalar loads).
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One block, persistent until idle.  `last` = the job number already done when
+// it starts (jobs are numbered from 1); `inc` = this incarnation's number.
+__global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* mb, uint64_t last, uint64_t inc,
+                                                                    uint64_t idle_ticks)
+{
+    __shared__ ResDesc s_d[kResMaxDescs];
+    __shared__ uint32_t s_pre[kResMaxDescs + 1];  // word prefix over the payload hulls
+    __shared__ uint64_t s_cmd;
+    const int t = threadIdx.x;
+    for (;;) {
+        if (t == 0) {
+            uint64_t cmd = 0;
+            const uint64_t t0 = wall_clock64();
+            for (;;) {
+                const uint64_t s = ld_sys(&mb->seq);
+                if (s != last) {
+                    cmd = s;
+                    break;
+                }
+                if (ld_sys(&mb->quit) || (uint64_t)(wall_clock64() - t0) > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_cmd = cmd;
+        }
+        __syncthreads();
+        const uint64_t cmd = s_cmd;
+        if (cmd == 0) break;  // every wave leaves together
+        // acquire at system scope: the job and the payloads the host wrote before
+        // the job number are read fresh, not from a cache
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t nd = ld_sys32(&mb->ndesc);
+        const uint32_t n = nd < (uint32_t)kResMaxDescs ? nd : (uint32_t)kResMaxDescs;
+        if (t < (int)n) s_d[t] = mb->desc[t];
+        __syncthreads();
+        if (t == 0) {
+            uint32_t w = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                s_pre[i] = w;
+                const ResDesc x = s_d[i];
+                w += x.len ? (uint32_t)(((x.addr + x.len + 15) >> 4) - (x.addr >> 4)) : 0u;
+            }
+            s_pre[n] = w;
+        }
+        __syncthreads();
+        const uint32_t total = s_pre[n];
+        for (uint32_t w0 = 0; w0 < total; w0 += kResBlock * kResWords) {
+            u32x4 v[kResWords];
+            uint32_t di[kResWords];
+#pragma unroll
+            for (int i = 0; i < kResWords; ++i) {
+                const uint32_t w = w0 + t + kResBlock * i;
+                di[i] = 0;
+                v[i] = u32x4{0, 0, 0, 0};
+                if (w < total) {
+                    uint32_t lo = 0, hi = n;  // last payload whose first word is <= w
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= w) lo = mid; else hi = mid;
+                    }
+                    di[i] = lo;
+                    const ResDesc x = s_d[lo];
+                    v[i] = *reinterpret_cast<const u32x4*>(((x.addr >> 4) + (w - s_pre[lo])) << 4);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kResWords; ++i) {
+                const uint32_t w = w0 + t + kResBlock * i;
+                if (w >= total) continue;
+                const ResDesc x = s_d[di[i]];
+                const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
+                const uint64_t end = x.addr + x.len;
+                const uint32_t r = rot_key(x.key, x.addr);
+                if (a >= x.addr && a + 16 <= end) {
+                    *reinterpret_cast<u32x4*>(a) = v[i] ^ r;
+                } else {  // a hull's first or last word: this payload's bytes only
+                    const uint64_t lo = a > x.addr ? a : x.addr, hi = a + 16 < end ? a + 16 : end;
+                    for (uint64_t q = lo; q < hi; ++q) {
+                        const uint32_t b = (uint32_t)(q - a);
+                        const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
+                        *reinterpret_cast<uint8_t*>(q) = (uint8_t)((dw ^ r) >> (8 * (b & 3u)));
+                    }
+                }
+            }
+        }
+        // release at system scope by every lane, then the job number: the host
+        // sees every payload byte before it sees `done`
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(&mb->done, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = cmd;
+    }
+    if (t == 0) __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+namespace {
+
+void quit_all_workers();
+
+// One per (host thread, device).  Never freed: releasing pinned memory from a
+// thread_local destructor can run after the HIP runtime was torn down.  At
+// process exit an atexit handler -- registered after the HIP runtime's own,
+// so it runs before the runtime's teardown -- asks every worker to quit and
+// waits (bounded) until each running kernel has exited: the grid has drained
+// before the process ends.  The idle exit ends a worker whose thread stopped
+// feeding.
+class ResidentWorker {
+public:
+    explicit ResidentWorker(int device) : device_(device) {}
+
+    // Ask the kernel to leave at its next poll and wait for it (atexit).
+    void quit_and_wait()
+    {
+        if (!mb_ || !running_) return;
+        __atomic_store_n(&mb_->quit, 1ull, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) != inc_ &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500))
+            cpu_relax();
+    }
+
+    bool usable()
+    {
+        if (state_ == 0) state_ = init() == KMWS_OK ? 1 : -1;
+        return state_ == 1 && enabled_;
+    }
+    void set_enabled(bool on) { enabled_ = on; }
+
+    // One synchronous job of n <= kResMaxDescs payloads.
+    kmws_status run(const ResDesc* d, uint32_t n)
+    {
+        if (n == 0) return KMWS_OK;
+        if (!usable() || n > (uint32_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
+        const uint64_t inc_exited = __atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE);
+        if (!running_ || inc_exited == inc_) {
+            kmws_status st = launch(seq_);  // every earlier job is done
+            if (st != KMWS_OK) return st;
+        }
+        std::memcpy(mb_->desc, d, n * sizeof(ResDesc));
+        mb_->ndesc = n;
+        const uint64_t s = ++seq_;
+        __atomic_store_n(&mb_->seq, s, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0;; ++spin) {
+            if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
+            cpu_relax();
+            if ((spin & 255) != 255) continue;
+            if (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) == inc_) {
+                // idle exit raced with this job: done is written before exited
+                if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
+                kmws_status st = launch(s - 1);  // the new incarnation takes job s
+                if (st != KMWS_OK) return st;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                // The job may still run later, so it is not retried (XOR twice is
+                // the identity): the call fails, and this worker is never used
+                // again (later calls launch kernels on their own streams).
+                __atomic_store_n(&mb_->quit, 1ull, __ATOMIC_RELEASE);
+                state_ = -1;
+                return KMWS_ERR_FAILED;
+            }
+        }
+        ++jobs_;
+        return KMWS_OK;
+    }
+
+    uint64_t jobs() const { return jobs_; }
+    uint64_t launches() const { return inc_; }
+    int running()
+    {
+        return running_ && __atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) != inc_ ? 1 : 0;
+    }
+
+private:
+    kmws_status init()
+    {
+        if (device_ < 0 || kmws_device_count() <= device_) return KMWS_ERR_NOT_SUPPORTED;
+        DevGuard g(device_);
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(ResMailbox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            return KMWS_ERR_FAILED;
+        }
+        mb_ = static_cast<ResMailbox*>(p);
+        std::memset(static_cast<void*>(mb_), 0, sizeof(ResMailbox));
+        dmb_ = static_cast<ResMailbox*>(device_view(mb_));
+        if (!dmb_) return KMWS_ERR_FAILED;
+        // a CU-masked stream gets a hardware queue of its own (the mask is a queue
+        // property): kernels of other streams never wait behind the resident one
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_) != hipSuccess || ncu <= 0)
+            return KMWS_ERR_FAILED;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
+        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+        if (hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            return KMWS_ERR_FAILED;
+        }
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0)
+            khz = 100000;  // gfx9 constant clock: 100 MHz
+        idle_ticks_ = (uint64_t)khz * kResIdleMs;
+        // registered after the HIP runtime initialised (the calls above), so at
+        // exit it runs before the runtime's own teardown
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(quit_all_workers); });
+        return KMWS_OK;
+    }
+
+    kmws_status launch(uint64_t last)
+    {
+        DevGuard g(device_);
+        ++inc_;
+        hipLaunchKernelGGL(resident_unmask_kernel, dim3(1), dim3(kResBlock), 0, stream_, dmb_, last, inc_,
+                           idle_ticks_);
+        if (hipGetLastError() != hipSuccess) {
+            state_ = -1;
+            return KMWS_ERR_FAILED;
+        }
+        running_ = true;
+        return KMWS_OK;
+    }
+
+    int device_;
+    int state_ = 0;  // 0 untried, 1 ready, -1 unusable
+    bool enabled_ = true;
+    bool running_ = false;
+    ResMailbox* mb_ = nullptr;
+    ResMailbox* dmb_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    uint64_t idle_ticks_ = 0;
+    uint64_t seq_ = 0, inc_ = 0, jobs_ = 0;
+};
+
+// Every worker of the process (for the exit handler); never freed.
+std::mutex g_all_mu;
+std::vector<ResidentWorker*>* g_all = nullptr;
+
+void quit_all_workers()
+{
+    std::lock_guard<std::mutex> lk(g_all_mu);
+    if (g_all)
+        for (ResidentWorker* w : *g_all) w->quit_and_wait();
+}
+
+ResidentWorker* worker(int device)
+{
+    static thread_local std::vector<ResidentWorker*> by_dev;
+    if (device < 0 || device > 1024) return nullptr;
+    if ((size_t)device >= by_dev.size()) by_dev.resize(device + 1, nullptr);
+    if (!by_dev[device]) {
+        ResidentWorker* w = new (std::nothrow) ResidentWorker(device);
+        if (!w) return nullptr;
+        std::lock_guard<std::mutex> lk(g_all_mu);
+        if (!g_all) g_all = new std::vector<ResidentWorker*>();
+        g_all->push_back(w);
+        by_dev[device] = w;
+    }
+    return by_dev[device];
+}
+
+}  // namespace
+
+// Synchronous unmask of host payloads (device-visible views of pinned memory)
+// through this thread's resident worker.  KMWS_ERR_NOT_SUPPORTED: the job does
+// not fit a worker job (or the worker is off / unusable); the caller launches.
+kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
+                            const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2)
+{
+    if (n + n2 > (size_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
+    ResidentWorker* w = worker(device);
+    if (!w || !w->usable()) return KMWS_ERR_NOT_SUPPORTED;
+    ResDesc job[kResMaxDescs];
+    uint64_t bytes = 0;
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i, ++k) {
+        job[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base + descs[i].off), descs[i].len, descs[i].key};
+        bytes += descs[i].len;
+    }
+    for (size_t i = 0; i < n2; ++i, ++k) {
+        job[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base2 + descs2[i].off), descs2[i].len, descs2[i].key};
+        bytes += descs2[i].len;
+    }
+    if (bytes > kResMaxBytes) return KMWS_ERR_NOT_SUPPORTED;
+    return w->run(job, (uint32_t)k);
+}
+
+}  // namespace kmws
+
+extern "C" {
+
+kmws_status kmws_resident_enable(int device, int on)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    w->set_enabled(on != 0);
+    return KMWS_OK;
+}
+
+kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, int* running)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    if (jobs) *jobs = w->jobs();
+    if (launches) *launches = w->launches();
+    if (running) *running = w->running();
+    return KMWS_OK;
+}
+
+}  // extern "C"

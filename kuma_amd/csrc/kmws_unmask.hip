@@ -16,6 +16,7 @@
 // of traffic per payload byte + 16 B per descriptor; no MFMA.
 #include "kmws_bench.h"
 #include "kmws_common.hpp"
+#include "kmws_frame_parse.hpp"
 
 // Uncapped split grids (batches of frames shorter than a tile, the LDS-staged
 // path) load the tile's descriptors before its payload: cfg4's in-place unmask
@@ -82,6 +83,40 @@ __global__ void __launch_bounds__(kBlock) tile_map_kernel(const kmws_desc* __res
     const uint64_t b1 = (next + T - 1) >> tile_shift;
     for (uint64_t b = b0; b < b1; ++b) map[b] = f;
     if (f == n - 1) map[b1] = f;  // sentinel after the last tile: "next tile's frame" of the last tile
+}
+
+// Descriptor-indexed decode and the unmask plan in one pass
+// (kmws_unpack_unmask): lane f parses frame f's header (unpack_one: out_desc,
+// flags, err) and writes the tile map over its region [hdr_off[f],
+// hdr_off[f+1]) -- from 0 for the first frame, to the span for the last.  The
+// regions partition the wire and each frame's payload lies inside its own
+// (unpack_one rejects a frame that overruns the next header), so the map means
+// what tile_map_kernel's does, with no 16-byte descriptor round trip and no
+// second launch over the batch.  Offsets out of order or past the wire set
+// kStatusBadDesc (the apply then stores nothing); a header error sets
+// kStatusBadHeader and leaves that frame empty (the others are unmasked).
+__global__ void __launch_bounds__(kBlock) unpack_plan_kernel(const uint8_t* __restrict__ wire, uint64_t span,
+                                                             const uint64_t* __restrict__ hdr_off, uint32_t n,
+                                                             int mode, kmws_desc* __restrict__ out_desc,
+                                                             uint16_t* __restrict__ out_flags,
+                                                             uint8_t* __restrict__ out_err, uint32_t tile_shift,
+                                                             uint32_t* __restrict__ map, WsHead* __restrict__ head)
+{
+    const uint32_t f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n) return;
+    unpack_one(wire, span, hdr_off, n, f, mode, out_desc, out_flags, out_err, head);
+    const uint64_t h = hdr_off[f];
+    const uint64_t next = f + 1 < n ? hdr_off[f + 1] : span;
+    if (h > next || next > span) {
+        atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    const uint64_t start = f == 0 ? 0 : h;
+    const uint64_t T = 1ull << tile_shift;
+    const uint64_t b0 = (start + T - 1) >> tile_shift;
+    const uint64_t b1 = (next + T - 1) >> tile_shift;
+    for (uint64_t b = b0; b < b1; ++b) map[b] = f;
+    if (f == n - 1) map[b1] = f;  // sentinel after the last tile
 }
 
 // Issue every payload load of a tile.  Full tiles load unconditionally so the
@@ -262,7 +297,7 @@ __global__ void __launch_bounds__(kBlock) unmask_tail_kernel(uint8_t* __restrict
     u32x4 v[V];
     load_tile<V, false>(base, tile_lo, span, v);
     __builtin_amdgcn_sched_barrier(0);
-    finish_tile<V, false>(base, tile_lo, span, d, n, map, tile, head->status == 0, v, s_off, s_end, s_key);
+    finish_tile<V, false>(base, tile_lo, span, d, n, map, tile, (head->status & kStatusBadDesc) == 0, v, s_off, s_end, s_key);
 }
 
 // One block per full tile, blocks dealt over `k` equal parts of the span:
@@ -316,7 +351,7 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
         if (fi < n && fi <= fl) pre = *reinterpret_cast<const u32x4*>(d + fi);
         load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
         __builtin_amdgcn_sched_barrier(0);
-        finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+        finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, (head->status & kStatusBadDesc) == 0, v, s_off, s_end,
                                       s_key, &pre);
         return;
     }
@@ -324,7 +359,7 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
     // the status is read after the payload loads: its latency hides under theirs
-    finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, head->status == 0, v, s_off, s_end,
+    finish_tile<V, true, TWO, NT>(base, lo, lo + Cfg::kTile, d, n, map, tile, (head->status & kStatusBadDesc) == 0, v, s_off, s_end,
                                   s_key);
 }
 
@@ -680,6 +715,30 @@ kmws_status kmws_unmask_apply_sched(uint8_t* base, uint64_t span, const kmws_des
 }
 
 int kmws_unmask_default_schedule(uint64_t span, uint32_t n) { return (int)default_schedule(span, n); }
+
+kmws_status kmws_unpack_unmask(uint8_t* wire, uint64_t wire_len, const uint64_t* hdr_off, uint32_t n, int mode,
+                               kmws_desc* out_desc, uint16_t* out_flags, uint8_t* out_err, void* workspace,
+                               size_t workspace_bytes, int schedule, void* stream)
+{
+    if (bad_args(wire, out_desc, n, workspace) || (n && !hdr_off) ||
+        (mode != KMWS_MODE_CLIENT && mode != KMWS_MODE_SERVER))
+        return KMWS_ERR_INVALID_PARAM;
+    const uint32_t code = schedule < 0 ? default_schedule(wire_len, n) : (uint32_t)schedule;
+    if (!valid_schedule(code)) return KMWS_ERR_INVALID_PARAM;
+    uint64_t ntiles = 0;
+    kmws_status st = check_ws(wire_len, workspace_bytes, &ntiles);
+    if (st != KMWS_OK) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    WsHead* head = static_cast<WsHead*>(workspace);
+    if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
+    if (n == 0) return KMWS_OK;
+    hipLaunchKernelGGL(unpack_plan_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, wire, wire_len, hdr_off,
+                       n, mode, out_desc, out_flags, out_err, ilog2_u64(ProdCfg::kTile),
+                       reinterpret_cast<uint32_t*>(head + 1), head);
+    st = hip_status(hipGetLastError());
+    if (st != KMWS_OK) return st;
+    return launch_apply(code, wire, wire_len, out_desc, n, workspace, workspace_bytes, s);
+}
 
 // Times each schedule on the caller's batch, twice per schedule (XOR applied
 // twice is the identity, so the payload is unchanged on return), and returns

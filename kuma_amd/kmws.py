@@ -35,6 +35,7 @@ EXPORTS = [
     "kmws_copy_workspace_size", "kmws_encode_batch",
     "kmws_unpack_workspace_size", "kmws_unpack_headers", "kmws_gather_unmask", "kmws_find_headers",
     "kmws_pack_headers_workspace_size", "kmws_pack_headers", "kmws_find_headers_streams",
+    "kmws_unpack_unmask", "kmws_unpack_gather",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
     "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain", "kmws_rx_batch_submit",
@@ -46,7 +47,7 @@ EXPORTS = [
 #: every function include/kmws_bench.h declares (bench / test support, same library)
 BENCH_EXPORTS = [
     "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
-    "kmws_check_unmasked",
+    "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info",
 ]
 
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
@@ -123,6 +124,8 @@ def lib() -> C.CDLL:
         "kmws_arena_place": (C.c_int64, [u8p, u64, u64, u64, vp, C.POINTER(C.c_float), u32]),
         "kmws_fill_uniform_descs": (i32, [vp, u32, u64, u32, u64, vp]),
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
+        "kmws_resident_enable": (i32, [i32, i32]),
+        "kmws_resident_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
         "kmws_encode_batch": (i32, [u8p, vp, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_unpack_workspace_size": (sz, []),
@@ -131,6 +134,8 @@ def lib() -> C.CDLL:
         "kmws_find_headers_streams": (i32, [u8p, u64, vp, u32, vp, u32, vp, vp, vp]),
         "kmws_unpack_headers": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, vp]),
         "kmws_gather_unmask": (i32, [u8p, vp, u32, u8p, u64, vp, vp, sz, vp]),
+        "kmws_unpack_unmask": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, vp, sz, i32, vp]),
+        "kmws_unpack_gather": (i32, [u8p, u64, vp, u32, i32, vp, vp, vp, u8p, u64, vp, vp, sz, vp]),
         "kmws_pipeline_create": (vp, [i32, u64, u32, i32]),
         "kmws_pipeline_destroy": (None, [vp]),
         "kmws_mask_host_chain": (i32, [vp, vp, vp, sz, i32]),
@@ -310,6 +315,19 @@ class WSHandler:
         return lib().kmws_decoder_feed_deferred(self._d, batch._b, buf, n, self._tramp, None)
 
     encodeFrameHeader = staticmethod(encode_frame_header)
+
+
+def resident_info(device: int = 0) -> dict:
+    """kmws_resident_info of the calling thread's resident worker."""
+    jobs, launches, running = C.c_uint64(0), C.c_uint64(0), C.c_int(0)
+    _check(lib().kmws_resident_info(device, C.byref(jobs), C.byref(launches), C.byref(running)),
+           "kmws_resident_info")
+    return {"jobs": jobs.value, "launches": launches.value, "running": bool(running.value)}
+
+
+def resident_enable(on: bool, device: int = 0) -> None:
+    """kmws_resident_enable for the calling thread (False: a launch per sync call)."""
+    _check(lib().kmws_resident_enable(device, int(bool(on))), "kmws_resident_enable")
 
 
 def handle_data_mask(key: bytes, segments, device: int = 0) -> None:
@@ -726,6 +744,52 @@ def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
     _check(lib().kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), n, dst.data_ptr(),
                                     dst.numel(), dst_off.data_ptr(), ws.ptr, ws.nbytes,
                                     _stream_handle(stream)), "kmws_gather_unmask")
+
+
+def _opt(t):
+    return t.data_ptr() if t is not None else None
+
+
+def unpack_unmask(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: Workspace,
+                  wire_len: Optional[int] = None, schedule: Optional[int] = None, stream=None) -> None:
+    """kmws_unpack_unmask: header parse + unmask plan in one kernel, then the
+    in-place unmask of the wire (ws: unmask_workspace_size(wire_len))."""
+    wire_len = wire.numel() if wire_len is None else wire_len
+    n = hdr_off.shape[0]
+    dev = wire.device
+    _check_tensor(hdr_off, "hdr_off", 8, dev, n)
+    _check_tensor(out_desc, "out_desc", 8, dev, 2 * n)
+    if out_flags is not None:
+        _check_tensor(out_flags, "out_flags", 2, dev, n)
+    if out_err is not None:
+        _check_tensor(out_err, "out_err", 1, dev, n)
+    if wire.numel() < wire_len:
+        raise ValueError("wire shorter than wire_len")
+    _check(lib().kmws_unpack_unmask(wire.data_ptr(), wire_len, hdr_off.data_ptr(), n, mode, out_desc.data_ptr(),
+                                    _opt(out_flags), _opt(out_err), ws.ptr, ws.nbytes, _sched_arg(ws, schedule),
+                                    _stream_handle(stream)), "kmws_unpack_unmask")
+
+
+def unpack_gather(wire, hdr_off, mode: int, out_desc, out_flags, out_err, dst, dst_off, ws: Workspace,
+                  wire_len: Optional[int] = None, stream=None) -> None:
+    """kmws_unpack_gather: header parse inside the gather's scan, then the
+    payloads unmasked densely into dst (ws: copy_workspace_size(n, dst.numel()))."""
+    wire_len = wire.numel() if wire_len is None else wire_len
+    n = hdr_off.shape[0]
+    dev = wire.device
+    _check_tensor(hdr_off, "hdr_off", 8, dev, n)
+    _check_tensor(out_desc, "out_desc", 8, dev, 2 * n)
+    if out_flags is not None:
+        _check_tensor(out_flags, "out_flags", 2, dev, n)
+    if out_err is not None:
+        _check_tensor(out_err, "out_err", 1, dev, n)
+    _check_tensor(dst, "dst", 1, dev)
+    _check_tensor(dst_off, "dst_off", 8, dev, n + 1)
+    if wire.numel() < wire_len:
+        raise ValueError("wire shorter than wire_len")
+    _check(lib().kmws_unpack_gather(wire.data_ptr(), wire_len, hdr_off.data_ptr(), n, mode, out_desc.data_ptr(),
+                                    _opt(out_flags), _opt(out_err), dst.data_ptr(), dst.numel(), dst_off.data_ptr(),
+                                    ws.ptr, ws.nbytes, _stream_handle(stream)), "kmws_unpack_gather")
 
 
 def find_headers_into(buf, out) -> tuple:

@@ -126,3 +126,36 @@ def test_loopback_cfg1_adapter_batched(tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["verified"] and d["frames"] == 1000 and d["mode"] == "adapter"
+
+
+def _build_sync(tmp_path):
+    """tests/cpp/sync_cfg1.cpp: the synchronous drop-in vs
+    kuma's codec restated in oracle/, in process, one call per 64 KiB read / per send."""
+    lib = kb.build()
+    from oracle import oracle as orc
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    exe = tmp_path / "sync_cfg1"
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "sync_cfg1.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", str(exe)])
+    return exe
+
+
+def test_sync_program_builds(tmp_path):
+    assert _build_sync(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_sync_cfg1_resident_drop_in(tmp_path):
+    """cfg1 decoded synchronously per 64 KiB read and handleDataMask per send,
+    through the resident worker and through a launch per call: every payload
+    and masked buffer exact (speed is recorded by tools/bench_configs.py)."""
+    import json
+    r = subprocess.run([str(_build_sync(tmp_path)), "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert all(x["verified"] for x in rows)
+    assert {(x["case"], x["codec"]) for x in rows} >= {("decode_sync", "kmws_resident"), ("decode_sync", "kmws_launch"),
+                                                       ("mask_sync", "kmws_resident")}

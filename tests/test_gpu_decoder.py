@@ -305,3 +305,104 @@ def test_max_frame_length_through_gpu_decoder(length, chunk):
         assert want[0][-1] == 0 and len(want[1]) == 2 and want[1][0][-1] == payload
     else:
         assert 6 in want[0] and want[1] == []
+
+
+# ---- the resident worker behind the synchronous entries (kmws_resident.hip) ----
+
+def test_sync_feed_runs_on_the_resident_worker():
+    """kmws_decoder_feed's GPU step goes to the thread's resident worker (no
+    launch per call): jobs are counted, every frame equals the oracle's, and
+    the same stream with the worker switched off (a launch per call) gives the
+    same bytes."""
+    stream = masked_stream(101, 40, sizes=(0, 1, 5, 125, 126, 1000, 4096, 20000, 65535))
+    before = kmws.resident_info()
+    want = run_oracle(stream, orc.SERVER, 65536, inplace=True)
+    got = run_kmws(stream, kmws.SERVER, 65536, inplace=True)
+    assert got == want
+    after = kmws.resident_info()
+    assert after["jobs"] > before["jobs"] and after["running"]
+    kmws.resident_enable(False)
+    try:
+        assert run_kmws(stream, kmws.SERVER, 65536, inplace=True) == want
+        assert kmws.resident_info()["jobs"] == after["jobs"]
+    finally:
+        kmws.resident_enable(True)
+
+
+def test_resident_worker_idles_out_and_relaunches():
+    """With no job for 5 ms the worker kernel exits by itself (the grid drains);
+    the next synchronous call relaunches it and is still exact."""
+    import time
+    key = bytes.fromhex("a1b2c3d4")
+    seg = bytearray(range(256)) * 16
+    kmws.handle_data_mask(key, [seg])
+    info = kmws.resident_info()
+    assert info["running"]
+    t0 = time.time()
+    while kmws.resident_info()["running"] and time.time() - t0 < 2.0:
+        time.sleep(0.01)
+    assert not kmws.resident_info()["running"]
+    kmws.handle_data_mask(key, [seg])  # back to the original bytes
+    assert seg == bytearray(range(256)) * 16
+    after = kmws.resident_info()
+    assert after["launches"] == info["launches"] + 1 and after["running"]
+
+
+def test_resident_worker_does_not_block_other_streams():
+    """The resident kernel runs on a CU-masked stream with a hardware queue of
+    its own: a kernel on torch's stream, launched while the worker sits waiting
+    for jobs, completes (stream synchronize) well inside the worker's 5 ms idle
+    wait.  A device-wide synchronize does wait for the worker, at most about
+    its idle time."""
+    import time
+    import torch
+    x = torch.ones(1 << 20, device="cuda")
+    s = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    lat = []
+    for _ in range(20):
+        kmws.handle_data_mask(b"\x01\x02\x03\x04", [bytearray(4096)])
+        t0 = time.perf_counter()
+        y = x * 2
+        s.synchronize()
+        lat.append(time.perf_counter() - t0)
+        running = kmws.resident_info()["running"]
+        assert running, lat  # it was resident the whole time
+    assert sorted(lat)[len(lat) // 2] < 0.002, lat
+    assert float(y.sum()) == 2 * (1 << 20)
+    kmws.handle_data_mask(b"\x01\x02\x03\x04", [bytearray(4096)])
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.05
+
+
+@pytest.mark.parametrize("n", [1, 3, 15, 16, 17, 1024, 4096, 65536, 65537, 300000, (1 << 20) + 5])
+def test_mask_host_chain_sizes_resident_and_launch(n):
+    """handleDataMask(key, data, len) at every size class through the resident
+    worker (<= 1 MiB) and beyond it (the launch path), against the oracle's
+    byte loop, at odd alignments inside a larger buffer."""
+    rng = random.Random(n)
+    key = bytes(rng.randrange(256) for _ in range(4))
+    buf = bytearray(rng.randrange(256) for _ in range(n + 37))
+    for off in (0, 3, 17):
+        seg = memoryview(buf)[off:off + n]
+        want = orc.mask_bytes(key, bytes(seg))
+        arr = bytearray(seg)
+        kmws.handle_data_mask(key, [arr])
+        assert bytes(arr) == want
+
+
+def test_resident_many_small_jobs_stay_exact():
+    """Thousands of back-to-back jobs (the steady state of a loop thread): each
+    1-64 byte payload masked twice returns to its original bytes, checked
+    against the oracle after the first pass."""
+    rng = random.Random(7)
+    for i in range(3000):
+        n = rng.randrange(1, 65)
+        key = bytes(rng.randrange(256) for _ in range(4))
+        data = bytes(rng.randrange(256) for _ in range(n))
+        a = bytearray(data)
+        kmws.handle_data_mask(key, [a])
+        assert bytes(a) == orc.mask_bytes(key, data), i
+        kmws.handle_data_mask(key, [a])
+        assert bytes(a) == data, i

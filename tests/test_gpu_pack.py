@@ -179,6 +179,115 @@ def test_unpack_gather_roundtrip(T, kind):
     assert b"".join(bytes(w2[int(o):int(o) + int(L)]) for o, L in zip(dd["off"], dd["len"])) == orig
 
 
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max", "large"])
+def test_fused_unpack_unmask_and_gather_equal_the_two_step_forms(T, kind):
+    """kmws_unpack_unmask (header parse writing the unmask plan
+    in one kernel, then the in-place unmask) and kmws_unpack_gather (header
+    parse inside the gather's scan) produce exactly what kmws_unpack_headers +
+    kmws_unmask_batch / kmws_gather_unmask produce -- descriptors, flags,
+    errors, the unmasked wire, the dense payloads and offsets -- and the
+    payloads equal the oracle decoder's, at an aligned and a shifted wire."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(zlib.crc32(f"fused-{kind}".encode()))
+    wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, kind, 300 if kind != "max" else 6)
+    hdr, used = kmws.find_headers(bytes(wire))
+    n = len(hdr)
+    rets, ofr = orc.decode_chunks(bytes(wire[:used]), orc.SERVER, 0)
+    want_pay = b"".join(f.payload for f in ofr)
+    d_hdr = T.tensor(hdr, dtype=T.int64, device="cuda")
+    W = len(wire)
+    for shift in (0, 16 * 3):
+        base = T.zeros(W + shift + 64, dtype=T.uint8, device="cuda")
+        base[shift:shift + W] = T.from_numpy(wire.copy()).cuda()
+        d_wire = base[shift:]
+        # two-step reference forms
+        od, of, oe = (T.zeros((n, 2), dtype=T.int64, device="cuda"), T.zeros(n, dtype=T.int16, device="cuda"),
+                      T.full((n,), 99, dtype=T.uint8, device="cuda"))
+        kmws.unpack_headers(d_wire, d_hdr, kmws.SERVER, od, of, oe, kmws.Workspace(16), wire_len=W)
+        total = int(od[:, 1].bitwise_and(0xFFFFFFFF).sum())
+        dst0 = T.zeros(total + 32, dtype=T.uint8, device="cuda")
+        doff0 = T.zeros(n + 1, dtype=T.int64, device="cuda")
+        kmws.gather_unmask(d_wire, od, dst0, doff0, kmws.Workspace(kmws.copy_workspace_size(n, dst0.numel())))
+        # fused gather
+        fd, ff, fe = (T.zeros((n, 2), dtype=T.int64, device="cuda"), T.zeros(n, dtype=T.int16, device="cuda"),
+                      T.full((n,), 99, dtype=T.uint8, device="cuda"))
+        dst1 = T.full((total + 32,), 0xEE, dtype=T.uint8, device="cuda")
+        dst1[total:] = 0
+        doff1 = T.zeros(n + 1, dtype=T.int64, device="cuda")
+        wsg = kmws.Workspace(kmws.copy_workspace_size(n, dst1.numel()))
+        kmws.unpack_gather(d_wire, d_hdr, kmws.SERVER, fd, ff, fe, dst1, doff1, wsg, wire_len=W)
+        T.cuda.synchronize()
+        assert wsg.status() == 0
+        assert T.equal(fd, od) and T.equal(ff, of) and T.equal(fe, oe) and int(oe.max()) == 0
+        assert T.equal(doff1, doff0) and T.equal(dst1, dst0)
+        assert bytes(dst1.cpu().numpy()[:total]) == want_pay
+        # fused in place
+        wire2 = base.clone()
+        fd2 = T.zeros((n, 2), dtype=T.int64, device="cuda")
+        fe2 = T.full((n,), 99, dtype=T.uint8, device="cuda")
+        wsm = kmws.Workspace(kmws.unmask_workspace_size(W))
+        kmws.unpack_unmask(wire2[shift:], d_hdr, kmws.SERVER, fd2, None, fe2, wsm, wire_len=W)
+        wire3 = base.clone()
+        kmws.unmask_batch(wire3[shift:], od, kmws.Workspace(kmws.unmask_workspace_size(W)), W)
+        T.cuda.synchronize()
+        assert wsm.status() == 0 and T.equal(fd2, od) and T.equal(fe2, oe)
+        assert T.equal(wire2, wire3)
+        w2 = wire2[shift:shift + W].cpu().numpy()
+        dd = od.cpu().numpy().view(orc.DESC_DTYPE).reshape(-1)
+        assert b"".join(bytes(w2[int(o):int(o) + int(L)]) for o, L in zip(dd["off"], dd["len"])) == want_pay
+
+
+def test_fused_decode_header_errors_and_bad_offsets(T):
+    """A bad header inside the batch: both fused forms report it per frame
+    (out_err, status bit 2), give it no payload, and still decode every other
+    frame; offsets out of order make kmws_unpack_unmask store nothing (bit 1)."""
+    from kuma_amd import kmws
+    rng = np.random.default_rng(5)
+    wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, "mixed", 60)
+    hdr, used = kmws.find_headers(bytes(wire))
+    n = len(hdr)
+    bad = n // 2
+    wire = wire.copy()
+    wire[hdr[bad] + 1] &= 0x7F  # clear the MASK bit: a SERVER must reject an unmasked non-empty frame
+    expect_err = 7 if lens[bad] > 0 else 0
+    d_hdr = T.tensor(hdr, dtype=T.int64, device="cuda")
+    W = len(wire)
+    d_wire = to_dev(T, wire)
+    od = T.zeros((n, 2), dtype=T.int64, device="cuda")
+    oe = T.full((n,), 99, dtype=T.uint8, device="cuda")
+    kmws.unpack_headers(d_wire, d_hdr, kmws.SERVER, od, None, oe, kmws.Workspace(16), wire_len=W)
+    T.cuda.synchronize()
+    assert int(oe[bad]) == expect_err
+    ref = d_wire.clone()
+    kmws.unmask_batch(ref, od, kmws.Workspace(kmws.unmask_workspace_size(W)), W)
+    w = d_wire.clone()
+    fd = T.zeros((n, 2), dtype=T.int64, device="cuda")
+    fe = T.full((n,), 99, dtype=T.uint8, device="cuda")
+    wsm = kmws.Workspace(kmws.unmask_workspace_size(W))
+    kmws.unpack_unmask(w, d_hdr, kmws.SERVER, fd, None, fe, wsm, wire_len=W)
+    T.cuda.synchronize()
+    assert T.equal(fd, od) and T.equal(fe, oe) and T.equal(w, ref)
+    assert wsm.status() == (2 if expect_err else 0)
+    total = int(od[:, 1].bitwise_and(0xFFFFFFFF).sum())
+    dst = T.zeros(total + 32, dtype=T.uint8, device="cuda")
+    doff = T.zeros(n + 1, dtype=T.int64, device="cuda")
+    wsg = kmws.Workspace(kmws.copy_workspace_size(n, dst.numel()))
+    kmws.unpack_gather(d_wire, d_hdr, kmws.SERVER, fd, None, fe, dst, doff, wsg, wire_len=W)
+    dst0 = T.zeros(total + 32, dtype=T.uint8, device="cuda")
+    doff0 = T.zeros(n + 1, dtype=T.int64, device="cuda")
+    kmws.gather_unmask(d_wire, od, dst0, doff0, kmws.Workspace(kmws.copy_workspace_size(n, dst0.numel())))
+    T.cuda.synchronize()
+    assert T.equal(fd, od) and T.equal(fe, oe) and T.equal(dst, dst0) and T.equal(doff, doff0)
+    assert wsg.status() == (2 if expect_err else 0)
+    # offsets out of order: nothing unmasked, bit 1
+    sw = d_hdr.clone()
+    sw[3], sw[4] = d_hdr[4], d_hdr[3]
+    w = d_wire.clone()
+    kmws.unpack_unmask(w, sw, kmws.SERVER, fd, None, fe, wsm, wire_len=W)
+    T.cuda.synchronize()
+    assert wsm.status() & 1 and T.equal(w, d_wire)
+
+
 def test_unpack_error_codes_match_reference(T):
     """Single-frame wires from the golden set: per-frame WSError == the
     reference decoder's return code for that frame."""

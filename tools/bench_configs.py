@@ -11,6 +11,10 @@ end-to-end (host-memory) rate.  One JSON line per config on stdout.
         header pack + mask, header unpack, in-place unmask; headers/s.
   e2e   host-resident 64 KiB-frame wire image (14-byte headers), in-place
         unmask through kmws_pipeline (pinned H2D -> kernel -> D2H).
+  sync  the synchronous drop-in on kuma's call pattern, in C++
+        (tests/cpp/sync_cfg1.cpp): cfg1 decoded per 64 KiB read and
+        handleDataMask per send at 1/4/64 KiB, kuma's codec (oracle) vs the
+        resident worker vs a launch per call.
 """
 from __future__ import annotations
 
@@ -45,6 +49,33 @@ def cfg1(reps: int):
     sys.path.insert(0, ROOT)
     import bench
     return bench.run_cfg1(reps)
+
+
+def sync(reps: int):
+    """tests/cpp/sync_cfg1.cpp, built here with g++ against the product library
+    and the oracle; its JSON lines gathered into one record."""
+    import subprocess
+    import tempfile
+    from kuma_amd import build as kb
+    from oracle import oracle as orc
+    lib = kb.build()
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    inc = os.path.join(ROOT, "include")
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "sync_cfg1")
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", inc, os.path.join(ROOT, "tests", "cpp", "sync_cfg1.cpp"),
+                               "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
+                               "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", exe])
+        r = subprocess.run([exe, str(reps)], capture_output=True, text=True, timeout=300)
+    rows = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    out = {"config": "sync", "rc": r.returncode, "cases": rows,
+           "note": "in-process C++ driver, one codec call per 64 KiB read (decode) / per send (mask); "
+                   "kuma_oracle = the oracle's restatement of kuma's codec on one core"}
+    for x in rows:
+        out.setdefault(x["case"], {}).setdefault(str(x.get("len", "cfg1")), {})[x["codec"]] = \
+            x.get("GiB_s") if x["case"] == "decode_sync" else x.get("us_per_call")
+    return out
 
 
 # ------------------------------------------------------------------ cfg3
@@ -165,6 +196,13 @@ def cfg3(reps: int, gib: float):
         kmws.gather_unmask(wire, out_desc, dst, dst_off, ws_g)
 
     t_dec = timed(torch, decode, reps, calls=3)
+    # the same decode with the header parse fused into the gather's scan (kmws_unpack_gather)
+    dst_f = torch.empty(P + 16, dtype=torch.uint8, device=dev)
+    dst_off_f = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    od_f = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    ws_gf = kmws.Workspace(kmws.copy_workspace_size(n, dst_f.numel()))
+    t_dec_f = timed(torch, lambda: kmws.unpack_gather(wire, hdr_off, kmws.SERVER, od_f, None, None, dst_f, dst_off_f,
+                                                      ws_gf, wire_len=P + H), reps, calls=3)
     t_unpack = timed(torch, lambda: kmws.unpack_headers(wire, hdr_off, kmws.SERVER, out_desc, out_flags,
                                                         out_err, ws_u, wire_len=P + H), reps, calls=20)
     assert ws_u.status() == 0 and ws_g.status() == 0 and int(out_err.max()) == 0
@@ -186,8 +224,16 @@ def cfg3(reps: int, gib: float):
         kmws.unmask_batch(wire, out_desc, ws_m, P + H)
 
     t_dip = timed(torch, decode_in_place, 2 * (reps // 2) + 2)  # even: the wire stays unmasked
+    # fused: header parse writing the unmask plan, then the apply (kmws_unpack_unmask)
+    ws_mf = kmws.Workspace(kmws.unmask_workspace_size(P + H))
+    ws_mf.schedule = sched
+    t_dip_f = timed(torch, lambda: kmws.unpack_unmask(wire, hdr_off, kmws.SERVER, od_f, None, None, ws_mf,
+                                                      wire_len=P + H), 2 * (reps // 2) + 2)  # even
     kmws.unmask_batch(wire, out_desc, ws_m, P + H)  # back to the masked wire image
-    ok = ok and ok_in_place
+    torch.cuda.synchronize()
+    ok_fused = (ws_gf.status() == 0 and ws_mf.status() == 0 and torch.equal(od_f, out_desc) and
+                torch.equal(dst_off_f, dst_off) and torch.equal(dst_f[:P], dst[:P]))
+    ok = ok and ok_in_place and ok_fused
     # encode in kuma's iovec form (sendWsFrame, WebSocketImpl.cpp:381-436): headers packed into
     # 16-B slots (kmws_pack_headers), payloads masked in place where they lie (kmws_unmask_batch)
     hslots = torch.empty(16 * n, dtype=torch.uint8, device=dev)
@@ -214,6 +260,10 @@ def cfg3(reps: int, gib: float):
                        "alg_GB_s": enc_bytes / t_enc / 1e9, "hbm_frac": enc_bytes / t_enc / 8e12},
             "decode_unpack_gather": {"ms": t_dec * 1e3, "payload_GiB_s": P / t_dec / 2**30,
                                      "alg_GB_s": dec_bytes / t_dec / 1e9, "hbm_frac": dec_bytes / t_dec / 8e12},
+            "decode_unpack_gather_fused": {"ms": t_dec_f * 1e3, "payload_GiB_s": P / t_dec_f / 2**30,
+                                           "alg_GB_s": dec_bytes / t_dec_f / 1e9,
+                                           "hbm_frac": dec_bytes / t_dec_f / 8e12,
+                                           "note": "kmws_unpack_gather: header parse inside the gather's scan"},
             "unpack_only": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
             "encode_iovec_in_place": {"ms": t_iov * 1e3, "payload_GiB_s": P / t_iov / 2**30, "schedule": sched_s,
                                       "hbm_frac": (2 * P + 59 * n) / t_iov / 8e12,
@@ -222,6 +272,10 @@ def cfg3(reps: int, gib: float):
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12},
             "decode_unpack_in_place": {"ms": t_dip * 1e3, "payload_GiB_s": P / t_dip / 2**30,
                                        "hbm_frac": (2 * P + H + 16 * n + 35 * n) / t_dip / 8e12},
+            "decode_unpack_in_place_fused": {"ms": t_dip_f * 1e3, "payload_GiB_s": P / t_dip_f / 2**30,
+                                             "hbm_frac": (2 * P + H + 16 * n + 35 * n) / t_dip_f / 8e12,
+                                             "note": "kmws_unpack_unmask: parse + plan in one kernel, then apply"},
+            "verified_fused": bool(ok_fused),
             "roundtrip_payload_GiB_s": P / (t_enc + t_dec) / 2**30, "verified": bool(ok),
             "note": "decode is descriptor-indexed: header offsets = the receiver's host parse (here wire_off)"}
 
@@ -501,6 +555,18 @@ def cfg4(reps: int, messages: int, placed: bool = True):
     # odd whatever --reps: the wire ends masked again, the state the placed copy
     # below starts from (its odd pass count then leaves it unmasked)
     t_unmask = timed(torch, lambda: kmws.unmask_batch(wire, out_desc, ws_m, P + H), 2 * (reps // 2) + 1)
+    # the descriptor-indexed decode in place: two-step (unpack + unmask) and fused (kmws_unpack_unmask)
+    t_dip = timed(torch, lambda: (kmws.unpack_headers(wire, hdr_off, kmws.SERVER, out_desc, out_flags, out_err,
+                                                      ws_u, wire_len=P + H),
+                                  kmws.unmask_batch(wire, out_desc, ws_m, P + H)), 2 * (reps // 2) + 2)  # even
+    od_f = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    ws_mf = kmws.Workspace(kmws.unmask_workspace_size(P + H))
+    ws_mf.schedule = sched
+    t_dip_f = timed(torch, lambda: kmws.unpack_unmask(wire, hdr_off, kmws.SERVER, od_f, None, None, ws_mf,
+                                                      wire_len=P + H), 2 * (reps // 2) + 2)  # even
+    torch.cuda.synchronize()
+    ok_fused = ws_mf.status() == 0 and bool(torch.equal(od_f, out_desc))
+    verified = verified and ok_fused
     placed_rec = None
     if placed:  # the same in-place unmask on a copy of the wire in a placement-probed arena (as bench.py)
         arena, pw, rec = placed_buffer(torch, kmws, P + H)
@@ -541,6 +607,11 @@ def cfg4(reps: int, messages: int, placed: bool = True):
                                   # desc 16 + flags 2 in, slot 16 + length 1 + wire offset 8 out
                                   "hbm_frac": 43 * n / t_hdr / 8e12, "timing": "20 calls back to back per event pair"},
             "unpack": {"ms": t_unpack * 1e3, "Mheaders_s": n / t_unpack / 1e6},
+            "decode_unpack_in_place": {"ms": t_dip * 1e3, "payload_GiB_s": P / t_dip / 2**30,
+                                       "hbm_frac": (2 * P + H + 51 * n) / t_dip / 8e12},
+            "decode_unpack_in_place_fused": {"ms": t_dip_f * 1e3, "payload_GiB_s": P / t_dip_f / 2**30,
+                                             "hbm_frac": (2 * P + H + 51 * n) / t_dip_f / 8e12,
+                                             "note": "kmws_unpack_unmask: parse + plan in one kernel, then apply"},
             "unmask_in_place": {"ms": t_unmask * 1e3, "payload_GiB_s": P / t_unmask / 2**30, "schedule": sched,
                                 "hbm_frac": (2 * P + 16 * n) / t_unmask / 8e12, "placed": placed_rec},
             "host_header_walk": {"frames": len(hdrs), "Mheaders_s": len(hdrs) / t_walk / 1e6},
@@ -593,7 +664,7 @@ def e2e(gib: float, chunk_mib: int, depth: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e"])
+    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e", "sync"])
     ap.add_argument("--cfg2b-frames", type=int, default=1 << 20)
     ap.add_argument("--cfg2b-header", type=int, default=14, help="bytes between payloads (14 = masked 64 KiB header)")
     ap.add_argument("--reps", type=int, default=5)
@@ -616,6 +687,8 @@ def main():
             r = cfg3_e2e(a.cfg3_gib, a.e2e_chunk_mib, min(a.reps, 3))
         elif w == "cfg4":
             r = cfg4(a.reps, a.cfg4_messages, a.placement == "probe")
+        elif w == "sync":
+            r = sync(max(a.reps, 10))
         else:
             r = e2e(a.e2e_gib, a.e2e_chunk_mib, a.e2e_depth)
         print(json.dumps(r), flush=True)
