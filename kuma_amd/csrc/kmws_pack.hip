@@ -521,28 +521,43 @@ __device__ uint64_t g_trace_pro[(1u << 16) * 8];
 #else
 #define KMWS_TRACE_PRO(ev) do { } while (0)
 #endif
+// The prologue's per-row part, shared by prologue_kernel and pack_rows_kernel:
+// row `row`'s frame offsets (written to start[]), its frames' unit geometry
+// (s_fu, unit slot bases s_ub relative to the row's first slot) and edge words
+// (s_edge, live counts s_ne), all in LDS.  Returns false (block-uniform) when
+// the output exceeds cap: the status is set and nothing may be written.
+struct RowLds {
+    FrameUnits fu[kBlock];
+    uint32_t ub[kBlock + 1];
+    u32x4 edge[kBlock * kEdgeWords];
+    uint8_t ne[kBlock];  // live edge words per frame
+    V2 w[kBlock / 64];
+};
+struct RowInfo {
+    uint64_t F0, S0, total;
+    uint32_t nf;
+};
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
-                                                          const kmws_desc* __restrict__ d,
-                                                          const uint16_t* __restrict__ flags, uint32_t n,
-                                                          uint64_t cap, WsHead* __restrict__ head,
-                                                          const V2* __restrict__ tiles, uint32_t ntiles,
-                                                          const V2* __restrict__ grp, uint64_t* __restrict__ start,
-                                                          UnitRec* __restrict__ rec, u32x4* __restrict__ edge)
+__device__ __forceinline__ bool row_prologue(uint32_t rid, const uint8_t* __restrict__ src,
+                                             const kmws_desc* __restrict__ d, const uint16_t* __restrict__ flags,
+                                             uint32_t n, uint64_t cap, WsHead* __restrict__ head,
+                                             const V2* __restrict__ tiles, uint32_t ntiles,
+                                             const V2* __restrict__ grp, uint64_t* __restrict__ start, RowLds& L,
+                                             RowInfo& ri)
 {
-    __shared__ FrameUnits s_fu[kBlock];
-    __shared__ uint32_t s_ub[kBlock + 1];
-    __shared__ u32x4 s_edge[kBlock * kEdgeWords];
-    __shared__ uint8_t s_ne[kBlock];  // live edge words per frame
-    __shared__ V2 s_w[kBlock / 64];
+    FrameUnits* s_fu = L.fu;
+    uint32_t* s_ub = L.ub;
+    u32x4* s_edge = L.edge;
+    uint8_t* s_ne = L.ne;
+    V2* s_w = L.w;
     const uint32_t t = threadIdx.x;
     KMWS_TRACE_PRO(0);
-    const uint64_t F0 = (uint64_t)blockIdx.x * kBlock;
+    const uint64_t F0 = (uint64_t)rid * kBlock;
     const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
     const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
     // totals, the row's prefix and the three frames' descriptors: one latency level
     const V2 tot = tiles[ntiles];
-    const V2 pre = tiles[blockIdx.x / kRowsPerTile] + grp[blockIdx.x];
+    const V2 pre = tiles[rid / kRowsPerTile] + grp[rid];
     const uint64_t total = tot.a;
     kmws_desc x[kPre];
     uint32_t fl[kPre];
@@ -554,9 +569,13 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
     const uint64_t r0 = off.a, uf = off.b, S0 = pre.b, uend = pre.b + row.b;
     KMWS_TRACE_PRO(1);
     if (t < nf) start[f] = r0;
+    ri.F0 = F0;
+    ri.S0 = S0;
+    ri.total = total;
+    ri.nf = nf;
     if (total > cap) {  // records would not fit the workspace; the copy waves see the status (block-uniform)
         if (F0 == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
-        return;
+        return false;
     }
     FrameGeom g[kPre];
     g[0] = geom_at<HEADERS>(x[0], fl[0], r0);
@@ -656,6 +675,48 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         }
     }
     __syncthreads();
+    return true;
+}
+
+// A unit record from its frame's geometry: unit m of frame F0 + j.
+__device__ __forceinline__ UnitRec make_rec(const FrameUnits& fu, uint32_t m, uint32_t f, WsHead* __restrict__ head)
+{
+    UnitRec r;
+    const uint32_t b = m * (uint32_t)kUnitWords;  // unit base - b0
+    auto rel = [&](uint32_t x) -> uint32_t {
+        return x <= b ? 0u : (x - b >= (uint32_t)kUnitWords ? (uint32_t)kUnitWords : x - b);
+    };
+    r.dst = 16u * (fu.b0 + b);
+    r.src = 16u * (fu.b0 + b) + fu.sdel;
+    r.f = f;
+    r.rk = fu.rk;
+    const uint32_t klo = rel(fu.olo), khi = rel(fu.ohi), ilo = rel(fu.ilo), ihi = rel(fu.ihi);
+    r.own = klo | fu.head_f << 12 | khi << 16;
+    r.inner = ilo | ihi << 16;
+    if (ilo - klo > fu.head_f)  // cannot happen
+        atomicOr(&head->status, kStatusBadDesc);
+    return r;
+}
+
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restrict__ src,
+                                                          const kmws_desc* __restrict__ d,
+                                                          const uint16_t* __restrict__ flags, uint32_t n,
+                                                          uint64_t cap, WsHead* __restrict__ head,
+                                                          const V2* __restrict__ tiles, uint32_t ntiles,
+                                                          const V2* __restrict__ grp, uint64_t* __restrict__ start,
+                                                          UnitRec* __restrict__ rec, u32x4* __restrict__ edge)
+{
+    __shared__ RowLds L;
+    RowInfo ri;
+    const uint32_t t = threadIdx.x;
+    if (!row_prologue<HEADERS>(blockIdx.x, src, d, flags, n, cap, head, tiles, ntiles, grp, start, L, ri)) return;
+    const uint64_t F0 = ri.F0, S0 = ri.S0;
+    const uint32_t nf = ri.nf;
+    const FrameUnits* s_fu = L.fu;
+    const uint32_t* s_ub = L.ub;
+    const u32x4* s_edge = L.edge;
+    const uint8_t* s_ne = L.ne;
     KMWS_TRACE_PRO(3);
     // edge words of the block's frames: one contiguous run, whole 128-byte lines
     // (the run starts on one: 256 frames x 80 B), skipping lines without a live
@@ -684,19 +745,7 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         const uint32_t m = sl - s_ub[lo];
         UnitRec r;
         if (m < fu.units) {
-            const uint32_t b = m * (uint32_t)kUnitWords;  // unit base - b0
-            auto rel = [&](uint32_t x) -> uint32_t {
-                return x <= b ? 0u : (x - b >= (uint32_t)kUnitWords ? (uint32_t)kUnitWords : x - b);
-            };
-            r.dst = 16u * (fu.b0 + b);
-            r.src = 16u * (fu.b0 + b) + fu.sdel;
-            r.f = (uint32_t)F0 + lo;
-            r.rk = fu.rk;
-            const uint32_t klo = rel(fu.olo), khi = rel(fu.ohi), ilo = rel(fu.ilo), ihi = rel(fu.ihi);
-            r.own = klo | fu.head_f << 12 | khi << 16;
-            r.inner = ilo | ihi << 16;
-            if (ilo - klo > fu.head_f)  // cannot happen
-                atomicOr(&head->status, kStatusBadDesc);
+            r = make_rec(fu, m, (uint32_t)F0 + lo, head);
         } else {
             r.dst = r.src = 0;
             r.f = r.rk = 0;
@@ -756,8 +805,10 @@ struct UnitRegs {
 // lane, lane 63 takes it from lane 0 of the next instruction, and the last
 // interior word from `ex`.  Edge words (composed by edge_block: [klo, ilo)
 // then [ihi, khi)): one per lane, index clamped.
+// fedge: the owning frame's kEdgeWords edge words (global: edge + f * kEdgeWords,
+// or the row's LDS copy in pack_rows_kernel).
 __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const uint8_t* __restrict__ src,
-                                           const u32x4* __restrict__ edge, UnitRegs& R)
+                                           const u32x4* __restrict__ fedge, UnitRegs& R)
 {
     const uint8_t* s0 = x.fast ? x.s0 : src;
     const uint32_t lo_k = x.fast ? x.ilo : 0u, hi_k = x.fast ? x.last : 0u;
@@ -774,7 +825,7 @@ __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const ui
     const uint32_t nhead = x.ilo - x.klo;
     uint32_t q = (uint32_t)lane < nhead ? lane : x.head_f + (lane - nhead);
     q = q < (uint32_t)kEdgeWords ? q : (uint32_t)kEdgeWords - 1;
-    R.sv = edge[(uint64_t)x.f * kEdgeWords + q];
+    R.sv = fedge[q];
 }
 
 __device__ __forceinline__ u32x4 readlane0(const u32x4& v)
@@ -883,8 +934,56 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     // Every load is issued before the first store (vmcnt also counts stores, so
     // a load issued after a store would make its wait cover that store too).
     UnitRegs R;
-    unit_issue(x, lane, src, edge, R);
+    unit_issue(x, lane, src, edge + (uint64_t)x.f * kEdgeWords, R);
     unit_finish(x, lane, dst, total, R);
+}
+
+// Small-frame batches (pack_rows_kernel): the prologue and the copy of one
+// 256-frame row in ONE block.  The row's unit geometry and edge words stay in
+// LDS and the block's own waves copy the row's units (wave w takes slots w,
+// w + 4, ...; a frame cursor per wave, no search), so the edge-word buffer
+// and the unit records never go through HBM (write + read: 2 x (80 + 32 x
+// units) bytes per frame, ~5 % of a 4 KiB fragment), there is no kernel
+// boundary between the two, and a row's boundary source lines are read by one
+// CU.  Load balance is a row's: batches of large frames keep the two-kernel
+// form (launch_copy_tail).  A bad batch (output over cap) stores nothing:
+// every block sees the same total before its first store.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                           const kmws_desc* __restrict__ d,
+                                                           const uint16_t* __restrict__ flags, uint32_t n,
+                                                           uint64_t cap, WsHead* __restrict__ head,
+                                                           const V2* __restrict__ tiles, uint32_t ntiles,
+                                                           const V2* __restrict__ grp, uint64_t* __restrict__ start)
+{
+    __shared__ RowLds L;
+    RowInfo ri;
+    if (!row_prologue<HEADERS>(blockIdx.x, src, d, flags, n, cap, head, tiles, ntiles, grp, start, L, ri)) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nf = ri.nf, ns = L.ub[nf];
+    const uint64_t total = ri.total;
+    uint32_t cur = 0;  // frame of the wave's current slot (slots ascend)
+    for (uint32_t sl = wave; sl < ns; sl += kBlock / 64) {
+        while (cur + 1 < nf && L.ub[cur + 1] <= sl) ++cur;
+        cur = __builtin_amdgcn_readfirstlane(cur);
+        const uint32_t m = sl - L.ub[cur];
+        const FrameUnits fu = L.fu[cur];
+        if (m >= fu.units) continue;  // slots past a frame's exact unit count
+        UnitRec r = make_rec(fu, m, (uint32_t)ri.F0 + cur, head);
+        r.dst = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r.dst >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)r.dst);
+        r.src = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r.src >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t)r.src);
+        r.rk = __builtin_amdgcn_readfirstlane(r.rk);
+        r.own = __builtin_amdgcn_readfirstlane(r.own);
+        r.inner = __builtin_amdgcn_readfirstlane(r.inner);
+        const UnitInfo x = decode_unit(r, true, src);
+        if (x.khi == 0) continue;
+        UnitRegs R;
+        unit_issue(x, lane, src, L.edge + cur * kEdgeWords, R);
+        unit_finish(x, lane, dst, total, R);
+    }
 }
 
 // ------------------------------ header unpack / validate ------------------------------
@@ -1314,12 +1413,22 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
     return launch_copy_tail<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
 }
 
-// The prologue and the copy grid, after the scan.
+// The prologue and the copy grid, after the scan: one fused launch
+// (pack_rows_kernel) when the mean region is small -- cap / n bounds it from
+// above -- else the prologue and the copy grid.
+#ifndef KMWS_PACK_ROWS_MAX_MEAN
+#define KMWS_PACK_ROWS_MAX_MEAN 16384  // bytes; 0 = always the two-kernel form (A/B builds)
+#endif
 template <bool HEADERS>
 static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t nt = (uint32_t)n_tiles(n);
+    if (KMWS_PACK_ROWS_MAX_MEAN > 0 && cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
+        hipLaunchKernelGGL(pack_rows_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, dst, d, flags,
+                           n, cap, c.head, c.tiles, nt, c.grp, start);
+        return hip_status(hipGetLastError());
+    }
     hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
                        c.head, c.tiles, nt, c.grp, start, c.rec, c.edge);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer

@@ -19,8 +19,8 @@
 // The worker exits by itself after kResIdleMs (5 ms) without a job (and on quit):
 // every wave reaches the exit, the grid drains, and a host thread that stops
 // feeding never leaves a kernel behind.  The next job relaunches it.  It runs
-// on a stream of its own created with a CU mask, which gets a hardware queue
-// of its own, so work on other streams never queues behind it.
+// on a non-blocking stream of its own, so work on other streams -- the legacy
+// default stream included -- does not queue behind it (tests/test_gpu_decoder.py).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -268,14 +268,12 @@ private:
         std::memset(static_cast<void*>(mb_), 0, sizeof(ResMailbox));
         dmb_ = static_cast<ResMailbox*>(device_view(mb_));
         if (!dmb_) return KMWS_ERR_FAILED;
-        // a CU-masked stream gets a hardware queue of its own (the mask is a queue
-        // property): kernels of other streams never wait behind the resident one
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_) != hipSuccess || ncu <= 0)
-            return KMWS_ERR_FAILED;
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0xFFFFFFFFu);
-        if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
-        if (hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        // A non-blocking stream: the legacy default stream (torch's current stream
+        // unless the caller picked another) waits for every blocking stream's
+        // work, which would include this kernel -- measured: a kernel on the null
+        // stream behind a CU-masked (blocking) worker stream waited out its idle
+        // time, 5.02 ms each time.
+        if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
             (void)hipGetLastError();
             return KMWS_ERR_FAILED;
         }

@@ -90,16 +90,22 @@ def gpu_encode(T, src, offs, lens, flags, keys, cap=None):
 
 @pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k", "max"])
 @pytest.mark.parametrize("aligned", [True, False])
-def test_encode_parity(T, kind, aligned):
+@pytest.mark.parametrize("room", [0, 20000])
+def test_encode_parity(T, kind, aligned, room):
+    """room = spare output capacity per frame: 0 takes the fused row kernel
+    (pack_rows_kernel) wherever the mean region is <= 16 KiB, 20000 forces the
+    prologue + copy-grid form (the kernel choice bounds the mean by cap / n)."""
     rng = np.random.default_rng(zlib.crc32(f"{kind}-{aligned}".encode()))
     n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6}[kind]
     lens, flags, keys = frames(rng, kind, n)
     src, offs = src_arena(rng, lens, aligned)
     want, want_off = orc.encode_batch(src, offs, lens, flags, keys)
-    got, off, st, total = gpu_encode(T, src, offs, lens, flags, keys)
+    got, off, st, total = gpu_encode(T, src, offs, lens, flags, keys,
+                                     cap=len(want) + room * n if room else None)
     assert st == 0 and total == len(want)
     assert np.array_equal(off[:n].astype(np.uint64), want_off) and off[n] == len(want)
     assert np.array_equal(got[:total], want)
+    assert (got[total:total + 16] == 0xEE).all()  # nothing written past the wire
 
 
 def test_encode_rejects_small_dst(T):
