@@ -125,6 +125,15 @@ void          kmws_decoder_reset(kmws_decoder* dec);                /* WSHandler
  * failed. */
 int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_cb cb, void* user);
 
+/* In-place contract of kmws_decoder_feed for a PAGEABLE chunk (on by default).
+ * Off: a masked payload lying in the chunk is delivered as a view of its
+ * unmasked pinned staging copy and the chunk keeps its masked bytes -- one
+ * host copy fewer per read.  kuma cannot tell the difference: its read buffer
+ * is not touched after handleData returns (TcpConnection.cpp:229-238) and the
+ * frame callback only sees the view (WSHandler.cpp:285).  Pinned chunks are
+ * always unmasked in place (zero-copy). */
+void kmws_decoder_set_in_place(kmws_decoder* dec, int on);
+
 /* WSHandler::handleDataMask(key, KMBuffer&) (WSHandler.cpp:312-322) and, with
  * nseg == 1, handleDataMask(key, data, len) (:303-310) for HOST buffers: the
  * segments of a chain are masked in place with the key phase continuing

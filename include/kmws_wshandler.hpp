@@ -196,6 +196,14 @@ public:
     // kmws_status of the last handleData: KMWS_OK, or why the GPU step failed
     int lastStatus() const { return st_->last_status; }
 
+    // kmws_decoder_set_in_place: false delivers masked payloads of a pageable
+    // read buffer as views of their unmasked staging copy (one host copy fewer;
+    // kuma does not read its buffer after handleData returns).
+    void setInPlace(bool on)
+    {
+        if (st_->dec) kmws_decoder_set_in_place(st_->dec, on ? 1 : 0);
+    }
+
     void setFrameCallback(FrameCallback cb) { st_->cb = std::move(cb); }  // WSHandler.h:46
 
     void reset()  // WSHandler.cpp:324-327

@@ -56,6 +56,7 @@ struct Pending {
 struct kmws_decoder {
     int mode = KMWS_MODE_CLIENT;
     int device = 0;
+    bool in_place = true;  // kmws_decoder_set_in_place
     // DecodeContext (WSHandler.h:66-78)
     kmws_frame_hdr hdr{};
     St state = St::HDR1;
@@ -298,6 +299,11 @@ void kmws_decoder_reset(kmws_decoder* dec)
     if (dec) dec->reset_ctx();
 }
 
+void kmws_decoder_set_in_place(kmws_decoder* dec, int on)
+{
+    if (dec) dec->in_place = on != 0;
+}
+
 // WSHandler::handleData (WSHandler.cpp:41-44, decodeFrame :108-280) in three
 // phases: (1) parse the chunk, collecting completed frames; (2) one GPU unmask
 // batch over their masked payloads -- in place in the caller's chunk when it
@@ -369,6 +375,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     }
 
     // ---- in-order delivery ----
+    const bool in_place = dec->in_place;  // the callbacks may destroy the decoder
     std::vector<Pending> todo;
     todo.swap(dec->pending);
     std::vector<std::vector<uint8_t>> held;
@@ -378,6 +385,10 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
         uint8_t* payload;
         switch (q.where) {
         case kInChunkStaged:  // unmasked in place in the caller's buffer, as kuma does (:260)
+            if (!in_place) {     // or the view points at the unmasked staging copy
+                payload = stage + q.stage_off;
+                break;
+            }
             std::memcpy(q.data_ptr, stage + q.stage_off, q.hdr.length);
             payload = q.data_ptr;
             break;

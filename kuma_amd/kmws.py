@@ -30,6 +30,7 @@ FLAG_MASK = 0x100
 EXPORTS = [
     "kmws_encode_header", "kmws_header_size", "kmws_decoder_create", "kmws_decoder_destroy",
     "kmws_decoder_set_mode", "kmws_decoder_reset", "kmws_decoder_feed", "kmws_device_count",
+    "kmws_decoder_set_in_place",
     "kmws_unmask_workspace_size", "kmws_unmask_batch", "kmws_unmask_plan", "kmws_unmask_apply",
     "kmws_unmask_autotune", "kmws_unmask_apply_sched", "kmws_unmask_default_schedule", "kmws_read_status",
     "kmws_copy_workspace_size", "kmws_encode_batch",
@@ -108,6 +109,7 @@ def lib() -> C.CDLL:
         "kmws_decoder_destroy": (None, [vp]),
         "kmws_decoder_set_mode": (None, [vp, i32]),
         "kmws_decoder_reset": (None, [vp]),
+        "kmws_decoder_set_in_place": (None, [vp, i32]),
         "kmws_decoder_feed": (i32, [vp, u8p, sz, FRAME_CB, vp]),
         "kmws_device_count": (i32, []),
         "kmws_unmask_workspace_size": (sz, [u64]),
@@ -291,6 +293,10 @@ class WSHandler:
 
     def reset(self) -> None:
         lib().kmws_decoder_reset(self._d)
+
+    def setInPlace(self, on: bool) -> None:
+        """kmws_decoder_set_in_place (default True)."""
+        lib().kmws_decoder_set_in_place(self._d, int(bool(on)))
 
     def handleData(self, data) -> int:
         n = len(data)

@@ -7,8 +7,10 @@
 //             kuma    the oracle's restatement of WSHandler::handleData;
 //             kmws    kmws::ws::WSHandler::handleData (kmws_decoder_feed) with
 //                     the thread's resident worker (no launch per read);
-//             launch  the same with the worker switched off (a kernel launch
-//                     and an event wait per read: round 3's form).
+//             views   the same, payloads delivered as views of the unmasked
+//                     staging copy (kmws_decoder_set_in_place(0)): no copy back;
+//             launch  the resident form with the worker switched off (a kernel
+//                     launch and an event wait per read: round 3's form).
 //   mask    WSHandler::handleDataMask(key, data, len) once per send
 //           (WebSocketImpl.cpp:388), 1 KiB, 4 KiB and 64 KiB payloads in a
 //           pageable buffer: the oracle's byte loop vs
@@ -151,12 +153,13 @@ int main(int argc, char** argv)
         emit_decode("kuma_oracle", t, reads, c, reps);
         ok &= c.bad == 0 && c.got == kFrames * (reps + 1);
     }
-    for (const char* codec : {"kmws_resident", "kmws_launch"}) {  // the drop-in, synchronous
-        const bool resident = std::string(codec) == "kmws_resident";
+    for (const char* codec : {"kmws_resident", "kmws_resident_views", "kmws_launch"}) {  // the drop-in, synchronous
+        const bool resident = std::string(codec) != "kmws_launch";
         kmws_resident_enable(0, resident ? 1 : 0);
         Check c{&plain};
         kmws::ws::WSHandler h;
         h.setMode(kmws::ws::WSMode::SERVER);
+        h.setInPlace(std::string(codec) != "kmws_resident_views");
         h.setFrameCallback([&](kmws::ws::FrameHeader, kmws::ws::BufferChain& b) {
             c.frame(static_cast<const uint8_t*>(b.readPtr()), b.length());
             return 0;

@@ -410,3 +410,22 @@ def test_resident_many_small_jobs_stay_exact():
         assert bytes(a) == orc.mask_bytes(key, data), i
         kmws.handle_data_mask(key, [a])
         assert bytes(a) == data, i
+
+
+def test_sync_feed_views_mode_leaves_chunk_masked():
+    """kmws_decoder_set_in_place(0): every frame (header fields and payload)
+    equals the oracle's, and the caller's pageable chunk keeps its masked
+    bytes (the payload views point at the unmasked staging copy)."""
+    stream = masked_stream(202, 60, sizes=(0, 1, 3, 125, 126, 4096, 20000, 65535, 70000))
+    want = run_oracle(stream, orc.SERVER, 65536)[:2]
+    h = kmws.WSHandler(kmws.SERVER)
+    h.setInPlace(False)
+    got = []
+    h.setFrameCallback(lambda hd, p: got.append(frame_key(hd, p)))
+    rets, chunks = [], []
+    for i in range(0, len(stream), 65536):
+        piece = bytearray(stream[i:i + 65536])
+        rets.append(h.handleData(piece))
+        chunks.append(bytes(piece))
+    assert (rets, got) == want
+    assert b"".join(chunks) == stream
