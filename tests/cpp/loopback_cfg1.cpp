@@ -11,6 +11,12 @@
 //        kmws_rx_batch_flush per loop iteration (socket drained to EAGAIN).
 //        The batches and rings belong to the loop threads (created once); the
 //        decoder is per connection, as kuma's WSHandler.
+//   sync  the plain member swap: the server holds a
+//        kmws::BasicWSHandler WITHOUT an RxLoop and calls handleData once per
+//        read into a pageable buffer, synchronously, like kuma's WSHandler (the
+//        thread's resident worker unmasks each read, no launch); the client masks
+//        each payload with the static handleDataMask (sendWsFrame,
+//        WebSocketImpl.cpp:388) and packs the header with encodeFrameHeader.
 //   adapter  the drop-in as kuma would run it: the server
 //        holds a kmws::BasicWSHandler (include/kmws_wshandler.hpp) in batched
 //        mode -- handleData per read, as WebSocket::Impl::onWsData calls it,
@@ -22,7 +28,7 @@
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu|adapter [reps] [frames per send iteration] [rx flush bytes]
+// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -145,6 +151,8 @@ struct LoopObjs {
 };
 
 // One connection: returns seconds from the first send to the last delivered frame.
+bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
+
 double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
     int ls = socket(AF_INET, SOCK_STREAM, 0);
@@ -168,7 +176,26 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         int one = 1;
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
         ready = true;
-        if (gpu && !adapter) {
+        if (g_sync) {
+            kmws::ws::WSHandler h;  // per connection; no RxLoop: one synchronous GPU job per read
+            h.setMode(kmws::ws::WSMode::SERVER);
+            h.setInPlace(false);
+            h.setFrameCallback([&e](kmws::ws::FrameHeader hdr, kmws::ws::BufferChain& buf) {
+                check_frame(&e, static_cast<const uint8_t*>(buf.readPtr()), buf.length(), hdr.opcode);
+                return 0;
+            });
+            std::vector<uint8_t> buf(kRead);  // kuma's read buffer (pageable)
+            while (e.got.load(std::memory_order_acquire) < kFrames) {
+                double t = now_s();
+                const ssize_t r = recv(fd, buf.data(), kRead, 0);
+                g_t.recv += now_s() - t;
+                if (r <= 0) break;
+                t = now_s();
+                const kmws::ws::WSError err = h.handleData(buf.data(), (size_t)r);
+                g_t.rx_feed += now_s() - t;
+                if (err != kmws::ws::WSError::NOERR && err != kmws::ws::WSError::NEED_MORE_DATA) std::exit(4);
+            }
+        } else if (gpu && !adapter) {
             kmws_decoder* d = kmws_decoder_create(KMWS_MODE_SERVER, 0);  // per connection, as in kuma
             kmws_rx_batch* b = lo.rx;
             uint8_t* ring = lo.rring;
@@ -275,7 +302,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     kmws_tx_batch* tx = lo.tx;
     uint8_t* sring = lo.sring;
     std::vector<uint8_t> sbuf;
-    if (!gpu) sbuf.resize(kGroup * kLen);
+    if (!gpu || g_sync) sbuf.resize(kGroup * kLen);
     std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hdrs(kGroup);
     std::vector<int> hlen(kGroup);
     std::vector<iovec> iov;
@@ -329,13 +356,23 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     }
     for (int g0 = 0; g0 < kFrames && !adapter; g0 += kGroup) {
         const int ng = std::min(kGroup, kFrames - g0);
-        uint8_t* base = gpu ? sring : sbuf.data();
+        uint8_t* base = gpu && !g_sync ? sring : sbuf.data();
         // the application writes its payloads (the send buffer is reused per iteration)
         std::memcpy(base, e.plain.data() + (size_t)g0 * kLen, (size_t)ng * kLen);
         for (int j = 0; j < ng; ++j) {
             uint8_t* p = base + (size_t)j * kLen;
             const uint32_t key = keys[g0 + j];
-            if (gpu) {
+            if (g_sync) {  // sendWsFrame with the drop-in's statics (WebSocketImpl.cpp:381-392)
+                kmws::ws::FrameHeader h;
+                std::memset(static_cast<void*>(&h), 0, sizeof h);
+                h.fin = 1;
+                h.opcode = KMWS_OP_TEXT;
+                h.mask = 1;
+                std::memcpy(h.maskey, &key, 4);
+                if (kmws::ws::WSHandler::handleDataMask(h.maskey, p, kLen) != KMWS_OK) std::exit(7);
+                h.length = (uint32_t)kLen;
+                hlen[j] = kmws::ws::WSHandler::encodeFrameHeader(h, hdrs[j].data());
+            } else if (gpu) {
                 kmws_frame_hdr h;
                 std::memset(&h, 0, sizeof h);
                 h.fin = 1;
@@ -357,7 +394,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             }
         }
         double tt = now_s();
-        if (gpu && kmws_tx_batch_flush(tx) != ng) std::exit(7);
+        if (gpu && !g_sync && kmws_tx_batch_flush(tx) != ng) std::exit(7);
         g_t.tx_flush += now_s() - tt;
         iov.clear();
         for (int j = 0; j < ng; ++j) {
@@ -384,7 +421,8 @@ int main(int argc, char** argv)
     if (argc > 3) kGroup = std::max(1, std::atoi(argv[3]));
     if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
     const bool adapter = mode == "adapter";
-    const bool gpu = mode == "gpu" || adapter;
+    g_sync = mode == "sync";
+    const bool gpu = mode == "gpu" || adapter || g_sync;
     if (gpu && kmws_device_count() < 1) {
         std::printf("{\"mode\": \"gpu\", \"error\": \"no gfx950 device\"}\n");
         return 1;

@@ -114,6 +114,18 @@ def test_loopback_cfg1_gpu_codec(tmp_path):
 
 
 @pytest.mark.gpu
+def test_loopback_cfg1_sync_member_swap(tmp_path):
+    """The plain member swap over loopback: the server's drop-in decodes each
+    read synchronously (resident worker), the client masks each send with the
+    drop-in's static handleDataMask; every payload delivered intact, in order."""
+    import json
+    r = subprocess.run([str(_build_loopback(tmp_path)), "sync", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["verified"] and d["frames"] == 1000 and d["mode"] == "sync"
+
+
+@pytest.mark.gpu
 def test_loopback_cfg1_adapter_batched(tmp_path):
     """The drop-in in batched mode over loopback: kmws::BasicWSHandler with an
     RxLoop (asynchronous submit / poll once per loop iteration) on the server,

@@ -78,6 +78,35 @@ def sync(reps: int):
     return out
 
 
+def loopback(reps: int):
+    """tests/cpp/loopback_cfg1.cpp over a real loopback socket (BASELINE
+    configs[0]): kuma's codec (oracle) on both ends vs the synchronous member
+    swap, the loop-batched gpu mode and the RxLoop adapter, 16 and 64 frames per
+    send iteration."""
+    import subprocess
+    import tempfile
+    from kuma_amd import build as kb
+    from oracle import oracle as orc
+    lib = kb.build()
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    inc = os.path.join(ROOT, "include")
+    rows = []
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "loopback_cfg1")
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-I", inc, os.path.join(ROOT, "tests", "cpp", "loopback_cfg1.cpp"),
+                               "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
+                               "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", exe])
+        for group in ("16", "64"):
+            for mode in ("cpu", "sync", "gpu", "adapter"):
+                r = subprocess.run([exe, mode, str(reps), group], capture_output=True, text=True, timeout=300)
+                rows += [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    out = {"config": "loopback_cfg1", "rows": rows}
+    for x in rows:
+        out.setdefault("GiB_s", {}).setdefault(str(x.get("frames_per_send_iteration")), {})[x["mode"]] = x.get("GiB_s")
+    return out
+
+
 # ------------------------------------------------------------------ cfg3
 def zipf_lens(rng, n):
     k = np.arange(14)
@@ -664,7 +693,7 @@ def e2e(gib: float, chunk_mib: int, depth: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e", "sync"])
+    ap.add_argument("which", nargs="+", choices=["cfg1", "cfg2b", "cfg3", "cfg3_e2e", "cfg4", "e2e", "sync", "loopback"])
     ap.add_argument("--cfg2b-frames", type=int, default=1 << 20)
     ap.add_argument("--cfg2b-header", type=int, default=14, help="bytes between payloads (14 = masked 64 KiB header)")
     ap.add_argument("--reps", type=int, default=5)
@@ -689,6 +718,8 @@ def main():
             r = cfg4(a.reps, a.cfg4_messages, a.placement == "probe")
         elif w == "sync":
             r = sync(max(a.reps, 10))
+        elif w == "loopback":
+            r = loopback(max(a.reps, 10))
         else:
             r = e2e(a.e2e_gib, a.e2e_chunk_mib, a.e2e_depth)
         print(json.dumps(r), flush=True)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 measurements on the current build, RUN_TAG=<tag> -> gpurun_out/<tag>/:
-#  configs.jsonl  tools/bench_configs.py sync cfg1 cfg3 cfg4 (plain allocations)
+#  configs.jsonl  tools/bench_configs.py sync loopback cfg1 cfg3 cfg4 (plain allocations)
 #  trace/ + breakdown_cfg4.txt  rocprofv3 kernel trace of cfg4 (per-kernel times)
 #  fetch/, write/ + pmc_cfg4_kernels.txt  FETCH_SIZE and WRITE_SIZE passes of cfg4
 #    (separate runs, --kernel-trace only beside --pmc)
@@ -11,7 +11,7 @@ TAG=${RUN_TAG:?set RUN_TAG}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 400 python3 tools/bench_configs.py ${CONFIGS:-sync cfg1 cfg3 cfg4} --placement plain \
+timeout -k 10 400 python3 tools/bench_configs.py ${CONFIGS:-sync loopback cfg1 cfg3 cfg4} --placement plain \
     > "$OUT/configs.jsonl" 2> "$OUT/configs.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$OUT/trace" -o run -- \
     python3 tools/bench_configs.py cfg4 --reps 3 --placement plain > "$OUT/trace_cfg4.jsonl" 2> "$OUT/trace.err" &&
