@@ -59,13 +59,15 @@ struct ResDesc {  // one payload: device-visible address, bytes, LE key of its f
 static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 
 // Pinned host memory, polled by the worker.  Host-written and device-written
-// words sit in different 128-byte lines.
+// words sit in different 128-byte lines.  The polled word carries everything
+// the worker needs before it reads the descriptors, so a job costs one PCIe
+// round trip to notice and one to read its descriptors: job number (bits
+// 0-39), payload count (40-47) and the quit bit (63).
+constexpr uint64_t kJobMask = (1ull << 40) - 1;
+constexpr uint64_t kQuitBit = 1ull << 63;
 struct alignas(256) ResMailbox {
-    uint64_t seq;   // job number, written last by the host (release)
-    uint64_t quit;  // nonzero: exit at the next poll
-    uint32_t ndesc;
-    uint32_t pad0;
-    uint64_t pad1[5];
+    uint64_t word;  // job | ndesc << 40 | quit << 63, written last by the host (release)
+    uint64_t pad1[7];
     ResDesc desc[kResMaxDescs];
     alignas(128) uint64_t done;    // job number finished (device, release: payloads visible)
     alignas(128) uint64_t exited;  // incarnation number of the worker that exited
@@ -74,10 +76,6 @@ struct alignas(256) ResMailbox {
 
 // Loads of host-written words bypass every cache (and are never scalar loads).
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -96,23 +94,25 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
             uint64_t cmd = 0;
             const uint64_t t0 = wall_clock64();
             for (;;) {
-                const uint64_t s = ld_sys(&mb->seq);
-                if (s != last) {
-                    cmd = s;
+                const uint64_t w = ld_sys(&mb->word);
+                if (w & kQuitBit) break;
+                if ((w & kJobMask) != last) {
+                    cmd = w;
                     break;
                 }
-                if (ld_sys(&mb->quit) || (uint64_t)(wall_clock64() - t0) > idle_ticks) break;
+                if ((uint64_t)(wall_clock64() - t0) > idle_ticks) break;
                 __builtin_amdgcn_s_sleep(2);
             }
+            // acquire at system scope (the CU's vector L1 and the L2): the
+            // descriptors and payloads the host wrote before the job word are
+            // read fresh; the other waves load after the barrier below
+            if (cmd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             s_cmd = cmd;
         }
         __syncthreads();
         const uint64_t cmd = s_cmd;
         if (cmd == 0) break;  // every wave leaves together
-        // acquire at system scope: the job and the payloads the host wrote before
-        // the job number are read fresh, not from a cache
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        const uint32_t nd = ld_sys32(&mb->ndesc);
+        const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
         const uint32_t n = nd < (uint32_t)kResMaxDescs ? nd : (uint32_t)kResMaxDescs;
         if (t < (int)n) s_d[t] = mb->desc[t];
         __syncthreads();
@@ -166,12 +166,13 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 }
             }
         }
-        // release at system scope by every lane, then the job number: the host
-        // sees every payload byte before it sees `done`
+        // release at system scope by every lane (each wave waits for its own
+        // stores and writes the L2 back), then the job number: the host sees
+        // every payload byte before it sees `done`
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(&mb->done, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        last = cmd;
+        if (t == 0) __hip_atomic_store(&mb->done, cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = cmd & kJobMask;
     }
     if (t == 0) __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -195,7 +196,7 @@ public:
     void quit_and_wait()
     {
         if (!mb_ || !running_) return;
-        __atomic_store_n(&mb_->quit, 1ull, __ATOMIC_RELEASE);
+        __atomic_store_n(&mb_->word, kQuitBit, __ATOMIC_RELEASE);
         const auto t0 = std::chrono::steady_clock::now();
         while (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) != inc_ &&
                std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500))
@@ -216,13 +217,12 @@ public:
         if (!usable() || n > (uint32_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
         const uint64_t inc_exited = __atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE);
         if (!running_ || inc_exited == inc_) {
-            kmws_status st = launch(seq_);  // every earlier job is done
+            kmws_status st = launch(seq_ & kJobMask);  // every earlier job is done
             if (st != KMWS_OK) return st;
         }
         std::memcpy(mb_->desc, d, n * sizeof(ResDesc));
-        mb_->ndesc = n;
-        const uint64_t s = ++seq_;
-        __atomic_store_n(&mb_->seq, s, __ATOMIC_RELEASE);
+        const uint64_t s = ++seq_ & kJobMask;
+        __atomic_store_n(&mb_->word, s | (uint64_t)n << 40, __ATOMIC_RELEASE);
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0;; ++spin) {
             if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
@@ -231,14 +231,14 @@ public:
             if (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) == inc_) {
                 // idle exit raced with this job: done is written before exited
                 if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
-                kmws_status st = launch(s - 1);  // the new incarnation takes job s
+                kmws_status st = launch((s - 1) & kJobMask);  // the new incarnation takes job s
                 if (st != KMWS_OK) return st;
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
                 // The job may still run later, so it is not retried (XOR twice is
                 // the identity): the call fails, and this worker is never used
                 // again (later calls launch kernels on their own streams).
-                __atomic_store_n(&mb_->quit, 1ull, __ATOMIC_RELEASE);
+                __atomic_store_n(&mb_->word, kQuitBit, __ATOMIC_RELEASE);
                 state_ = -1;
                 return KMWS_ERR_FAILED;
             }
