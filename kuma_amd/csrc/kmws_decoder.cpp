@@ -602,8 +602,9 @@ kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ri
 // (the phase continues across segments, WSHandler.cpp:312-322): segments in
 // the attached pinned ring are masked in place there, the others gathered
 // into pinned staging and copied back when the generation completes; one
-// launch per buffer.
-int64_t kmws_tx_batch_submit(kmws_tx_batch* b)
+// launch per buffer -- or, for a flush (sync), one synchronous job on the
+// thread's resident worker (kmws_resident.hip) when it fits one.
+static int64_t tx_submit(kmws_tx_batch* b, bool sync)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
     if (b->frames.empty()) return 0;
@@ -633,7 +634,10 @@ int64_t kmws_tx_batch_submit(kmws_tx_batch* b)
                 phase += g.len;
             }
         }
-        st = b->ring_descs.empty() ? s.launch() : s.launch(b->ring, b->ring_bytes, &b->ring_descs);
+        if (sync)
+            st = b->ring_descs.empty() ? s.run() : s.run(b->ring, b->ring_bytes, &b->ring_descs);
+        else
+            st = b->ring_descs.empty() ? s.launch() : s.launch(b->ring, b->ring_bytes, &b->ring_descs);
     }
     b->frames.clear();
     b->ring_descs.clear();
@@ -653,6 +657,8 @@ int64_t kmws_tx_batch_submit(kmws_tx_batch* b)
     b->stage = std::move(next);
     return b->inflight.back().ticket;
 }
+
+int64_t kmws_tx_batch_submit(kmws_tx_batch* b) { return tx_submit(b, false); }
 
 int kmws_tx_batch_poll(kmws_tx_batch* b, int64_t ticket, int wait)
 {
@@ -681,7 +687,7 @@ int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
     const int64_t nf = (int64_t)b->frames.size();
-    const int64_t t = kmws_tx_batch_submit(b);
+    const int64_t t = tx_submit(b, true);  // masked when it returns: the poll only copies back
     if (t < 0) return t;
     const int r = kmws_tx_batch_poll(b, b->next_ticket - 1, 1);
     if (r < 0) return r;
@@ -773,14 +779,17 @@ void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
             if (it.dec == dec) it.live = false;
 }
 
-int kmws_rx_batch_submit(kmws_rx_batch* b)
+// sync (a flush): one synchronous job on the thread's resident worker when it
+// fits one (else a launch and a wait), instead of an enqueued launch.
+static int rx_submit(kmws_rx_batch* b, bool sync)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
     if (b->flushing) return KMWS_ERR_INVALID_STATE;
     if (b->items.empty()) return 0;
     std::unique_ptr<PinnedStage> next = b->take_stage();
     if (!next) return KMWS_ERR_FAILED;
-    kmws_status st = b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs);
+    kmws_status st = sync ? b->stage->run(b->ring, b->ring_bytes, &b->ring_descs)
+                          : b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs);
     b->ring_descs.clear();
     if (st != KMWS_OK) {
         // nothing of this generation can be delivered masked: drop it
@@ -797,6 +806,8 @@ int kmws_rx_batch_submit(kmws_rx_batch* b)
     b->stage = std::move(next);
     return n;
 }
+
+int kmws_rx_batch_submit(kmws_rx_batch* b) { return rx_submit(b, false); }
 
 int kmws_rx_batch_poll(kmws_rx_batch* b, int wait)
 {
@@ -839,7 +850,7 @@ int kmws_rx_batch_poll(kmws_rx_batch* b, int wait)
 
 int kmws_rx_batch_flush(kmws_rx_batch* b)
 {
-    const int s = kmws_rx_batch_submit(b);
+    const int s = rx_submit(b, true);
     const int d = kmws_rx_batch_poll(b, 1);
     return s < 0 ? s : d;
 }

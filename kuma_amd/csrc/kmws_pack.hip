@@ -938,6 +938,17 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     unit_finish(x, lane, dst, total, R);
 }
 
+// A wave-uniform 64-bit value into scalar registers.  readfirstlane returns a
+// signed int: each half goes through uint32_t, or a low half with bit 31 set
+// would sign-extend over the high half (an output offset past 2 GiB became an
+// address near 2^64 -- an illegal access, caught by tools/diag_pack_rows.py).
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
+
 // Small-frame batches (pack_rows_kernel): the prologue and the copy of one
 // 256-frame row in ONE block.  The row's unit geometry and edge words stay in
 // LDS and the block's own waves copy the row's units (wave w takes slots w,
@@ -971,10 +982,8 @@ __global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __rest
         const FrameUnits fu = L.fu[cur];
         if (m >= fu.units) continue;  // slots past a frame's exact unit count
         UnitRec r = make_rec(fu, m, (uint32_t)ri.F0 + cur, head);
-        r.dst = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r.dst >> 32)) << 32) |
-                __builtin_amdgcn_readfirstlane((uint32_t)r.dst);
-        r.src = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r.src >> 32)) << 32) |
-                __builtin_amdgcn_readfirstlane((uint32_t)r.src);
+        r.dst = uniform64(r.dst);
+        r.src = uniform64(r.src);
         r.rk = __builtin_amdgcn_readfirstlane(r.rk);
         r.own = __builtin_amdgcn_readfirstlane(r.own);
         r.inner = __builtin_amdgcn_readfirstlane(r.inner);

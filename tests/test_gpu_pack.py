@@ -608,3 +608,38 @@ def test_batch_entries_empty_and_single(T, n):
     if n:
         assert int(out_err[0]) == 0
         assert bytes(dense.cpu().numpy()[:int(lens[0])]) == bytes(src[16:16 + int(lens[0])])
+
+
+@pytest.mark.parametrize("room", [0, 20000])
+def test_encode_4k_frames_past_4_gib(T, room):
+    """cfg4's shape (masked 4 KiB frames, 8-byte headers) at 1.1 M frames: the
+    output crosses 2 GiB and 4 GiB (an offset with bit 31 set was once
+    sign-extended in the fused row kernel).  room 0: pack_rows_kernel; 20000:
+    the prologue + copy-grid form.  Every byte and offset checked on the
+    device against a torch restatement of encodeFrameHeader + mask."""
+    from kuma_amd import kmws
+    n, L, H = (1 << 20) + (1 << 16), 4096, 8
+    src = T.empty(n * L + 16, dtype=T.uint8, device="cuda")
+    kmws.fill_synthetic(src, 7)
+    descs = T.empty((n, 2), dtype=T.int64, device="cuda")
+    kmws.fill_uniform_descs(descs, L, L, 11)
+    fl = T.full((n,), 0x182, dtype=T.int16, device="cuda")
+    cap = n * (L + H) + room * n
+    wire = T.full((cap + 16,), 0xEE, dtype=T.uint8, device="cuda")
+    woff = T.empty(n + 1, dtype=T.int64, device="cuda")
+    ws = kmws.Workspace(kmws.copy_workspace_size(n, cap))
+    assert kmws.lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), fl.data_ptr(), n, wire.data_ptr(), cap,
+                                        woff.data_ptr(), ws.ptr, ws.nbytes, kmws._stream_handle()) == 0
+    T.cuda.synchronize()
+    assert ws.status() == 0
+    assert T.equal(woff, T.arange(n + 1, device="cuda", dtype=T.int64) * (L + H))
+    keys = (descs[:, 1] >> 32) & 0xFFFFFFFF
+    kb = T.stack([(keys >> (8 * i)) & 0xFF for i in range(4)], 1).to(T.uint8)
+    hdr = T.tensor([0x82, 0xFE, L >> 8, L & 0xFF], dtype=T.uint8, device="cuda")
+    step = 1 << 16
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        w = wire[a * (L + H):b * (L + H)].view(b - a, L + H)
+        assert bool((w[:, :4] == hdr).all()) and T.equal(w[:, 4:8], kb[a:b]), a
+        assert T.equal(w[:, 8:], src[a * L:b * L].view(b - a, L) ^ kb[a:b].repeat(1, L // 4)), a
+    assert bool((wire[n * (L + H):n * (L + H) + 16] == 0xEE).all())
