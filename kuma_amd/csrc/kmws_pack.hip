@@ -949,6 +949,10 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v)
     return (uint64_t)hi << 32 | lo;
 }
 
+#ifndef KMWS_PACK_ROWS_PIPE
+#define KMWS_PACK_ROWS_PIPE 1  // two units in flight per wave (0: one; A/B builds)
+#endif
+
 // Small-frame batches (pack_rows_kernel): the prologue and the copy of one
 // 256-frame row in ONE block.  The row's unit geometry and edge words stay in
 // LDS and the block's own waves copy the row's units (wave w takes slots w,
@@ -975,6 +979,48 @@ __global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __rest
     const uint32_t nf = ri.nf, ns = L.ub[nf];
     const uint64_t total = ri.total;
     uint32_t cur = 0;  // frame of the wave's current slot (slots ascend)
+#if KMWS_PACK_ROWS_PIPE
+    // Two units in flight per wave: the next unit's loads are issued before the
+    // current unit is composed and stored (its wait then counts only the loads
+    // issued before the stores of the unit before it).
+    uint32_t sl = wave;
+    auto next = [&](UnitInfo& x, uint32_t& e) -> bool {
+        for (; sl < ns; sl += kBlock / 64) {
+            while (cur + 1 < nf && L.ub[cur + 1] <= sl) ++cur;
+            cur = __builtin_amdgcn_readfirstlane(cur);
+            const uint32_t m = sl - L.ub[cur];
+            const FrameUnits fu = L.fu[cur];
+            if (m >= fu.units) continue;
+            UnitRec r = make_rec(fu, m, (uint32_t)ri.F0 + cur, head);
+            r.dst = uniform64(r.dst);
+            r.src = uniform64(r.src);
+            r.rk = __builtin_amdgcn_readfirstlane(r.rk);
+            r.own = __builtin_amdgcn_readfirstlane(r.own);
+            r.inner = __builtin_amdgcn_readfirstlane(r.inner);
+            x = decode_unit(r, true, src);
+            if (x.khi == 0) continue;
+            e = cur * kEdgeWords;
+            sl += kBlock / 64;
+            return true;
+        }
+        return false;
+    };
+    UnitInfo xa, xb;
+    UnitRegs Ra, Rb;
+    uint32_t ea = 0, eb = 0;
+    if (!next(xa, ea)) return;
+    unit_issue(xa, lane, src, L.edge + ea, Ra);
+    for (;;) {
+        const bool hb = next(xb, eb);
+        if (hb) unit_issue(xb, lane, src, L.edge + eb, Rb);
+        unit_finish(xa, lane, dst, total, Ra);
+        if (!hb) break;
+        const bool ha = next(xa, ea);
+        if (ha) unit_issue(xa, lane, src, L.edge + ea, Ra);
+        unit_finish(xb, lane, dst, total, Rb);
+        if (!ha) break;
+    }
+#else
     for (uint32_t sl = wave; sl < ns; sl += kBlock / 64) {
         while (cur + 1 < nf && L.ub[cur + 1] <= sl) ++cur;
         cur = __builtin_amdgcn_readfirstlane(cur);
@@ -993,6 +1039,7 @@ __global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __rest
         unit_issue(x, lane, src, L.edge + cur * kEdgeWords, R);
         unit_finish(x, lane, dst, total, R);
     }
+#endif
 }
 
 // ------------------------------ header unpack / validate ------------------------------

@@ -16,7 +16,7 @@
 // makes its stores visible system-wide and writes the job number back; the
 // host spins on that word.  No launch, no completion signal, no interrupt.
 //
-// The worker exits by itself after kResIdleMs (5 ms) without a job (and on quit):
+// The worker exits by itself after kResIdleUs (200 us) without a job (and on quit):
 // every wave reaches the exit, the grid drains, and a host thread that stops
 // feeding never leaves a kernel behind.  The next job relaunches it.  It runs
 // on a non-blocking stream of its own, so work on other streams -- the legacy
@@ -37,12 +37,19 @@ namespace kmws {
 
 constexpr int kResBlock = 1024;  // 16 waves: 4 words each = 64 KiB of loads in flight
 constexpr int kResWords = 4;
-// Idle exit: short, because hipDeviceSynchronize (torch.cuda.synchronize) waits
-// for every stream of the device, this kernel's included (measured: a device
-// synchronize issued while a 50 ms-idle worker sat waiting took 50 ms); a loop
-// thread under load feeds far more often than this, and a worker that idled
-// out costs one launch, the price of every call without it.
-constexpr uint32_t kResIdleMs = 5;
+// Idle exit: short.  The runtime maps streams onto a few hardware queues
+// (GPU_MAX_HW_QUEUES, 4 on the box), so a kernel launched on a stream that
+// shares the worker's queue waits until the worker leaves; and
+// hipDeviceSynchronize (torch.cuda.synchronize) waits for every stream, the
+// worker's included (measured: a device synchronize behind a 50 ms-idle worker
+// took 50 ms; the loopback "gpu" mode, whose batches keep several streams, fell
+// from 2.0 to 0.57 GiB/s with a 5 ms idle).  A loop thread under load feeds far
+// more often than this; a worker that idled out costs one launch at the next
+// job, the price of every call without it.
+#ifndef KMWS_RESIDENT_IDLE_US
+#define KMWS_RESIDENT_IDLE_US 200
+#endif
+constexpr uint32_t kResIdleUs = KMWS_RESIDENT_IDLE_US;
 
 static inline void cpu_relax()
 {
@@ -280,7 +287,7 @@ private:
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0)
             khz = 100000;  // gfx9 constant clock: 100 MHz
-        idle_ticks_ = (uint64_t)khz * kResIdleMs;
+        idle_ticks_ = (uint64_t)khz * kResIdleUs / 1000u;
         // registered after the HIP runtime initialised (the calls above), so at
         // exit it runs before the runtime's own teardown
         static std::once_flag once;

@@ -28,7 +28,9 @@
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes]
+// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [noresident]
+// (noresident: both loop threads switch their resident worker off -- every GPU
+// job a launch and a wait, the A/B of kmws_resident.hip)
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -48,6 +50,7 @@
 #include <thread>
 #include <vector>
 
+#include "kmws_bench.h"
 #include "kmws_gpu.h"
 #include "kmws_wshandler.hpp"
 
@@ -152,6 +155,7 @@ struct LoopObjs {
 
 // One connection: returns seconds from the first send to the last delivered frame.
 bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
+bool g_noresident = false;
 
 double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
@@ -172,6 +176,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     std::chrono::steady_clock::time_point t_end;
 
     std::thread server([&] {
+        if (g_noresident) kmws_resident_enable(0, 0);
         int fd = accept(ls, nullptr, nullptr);
         int one = 1;
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -420,6 +425,8 @@ int main(int argc, char** argv)
     const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
     if (argc > 3) kGroup = std::max(1, std::atoi(argv[3]));
     if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
+    g_noresident = argc > 5 && std::string(argv[5]) == "noresident";
+    if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     const bool adapter = mode == "adapter";
     g_sync = mode == "sync";
     const bool gpu = mode == "gpu" || adapter || g_sync;

@@ -330,31 +330,31 @@ def test_sync_feed_runs_on_the_resident_worker():
 
 
 def test_resident_worker_idles_out_and_relaunches():
-    """With no job for 5 ms the worker kernel exits by itself (the grid drains);
+    """With no job for 200 us the worker kernel exits by itself (the grid drains);
     the next synchronous call relaunches it and is still exact."""
     import time
     key = bytes.fromhex("a1b2c3d4")
     seg = bytearray(range(256)) * 16
     kmws.handle_data_mask(key, [seg])
-    info = kmws.resident_info()
-    assert info["running"]
     t0 = time.time()
     while kmws.resident_info()["running"] and time.time() - t0 < 2.0:
         time.sleep(0.01)
-    assert not kmws.resident_info()["running"]
+    info = kmws.resident_info()
+    assert not info["running"]  # left by itself
     kmws.handle_data_mask(key, [seg])  # back to the original bytes
     assert seg == bytearray(range(256)) * 16
     after = kmws.resident_info()
-    assert after["launches"] == info["launches"] + 1 and after["running"]
+    assert after["launches"] == info["launches"] + 1 and after["jobs"] == info["jobs"] + 1
 
 
 @pytest.mark.parametrize("which", ["default", "side"])
 def test_resident_worker_does_not_block_other_streams(which):
-    """The resident kernel runs on a non-blocking stream of its own: a kernel
-    on torch's default (legacy null) stream or on a side stream, launched while
-    the worker sits waiting for jobs, completes (stream synchronize) well
-    inside the worker's 5 ms idle wait.  A device-wide synchronize does wait
-    for the worker, at most about its idle time."""
+    """The resident kernel runs on a non-blocking stream of its own: while
+    another thread keeps its worker busy (resident the whole time), kernels on
+    torch's default (legacy null) stream or on a side stream complete
+    (stream synchronize) in well under a millisecond, not when the worker
+    leaves."""
+    import threading
     import time
     import torch
     x = torch.ones(1 << 20, device="cuda")
@@ -362,22 +362,34 @@ def test_resident_worker_does_not_block_other_streams(which):
     with torch.cuda.stream(s):
         y = x * 2  # the elementwise kernel's code object is loaded here, not in the timed loop
     torch.cuda.synchronize()
-    lat, resident = [], []
-    for _ in range(20):
-        kmws.handle_data_mask(b"\x01\x02\x03\x04", [bytearray(4096)])
-        t0 = time.perf_counter()
-        with torch.cuda.stream(s):
-            y = x * 2
-        s.synchronize()
-        lat.append(time.perf_counter() - t0)
-        resident.append(kmws.resident_info()["running"])  # resident the whole time
-    assert sum(resident) >= 15, (lat, resident)
+    stop = threading.Event()
+    busy = {"jobs": 0, "resident": False}
+
+    def feeder():
+        buf = bytearray(4096)
+        while not stop.is_set():
+            kmws.handle_data_mask(b"\x01\x02\x03\x04", [buf])
+            busy["jobs"] += 1
+            busy["resident"] = busy["resident"] or kmws.resident_info()["running"]
+
+    th = threading.Thread(target=feeder)
+    th.start()
+    try:
+        while busy["jobs"] < 100:
+            time.sleep(0.001)
+        lat = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            with torch.cuda.stream(s):
+                y = x * 2
+            s.synchronize()
+            lat.append(time.perf_counter() - t0)
+    finally:
+        stop.set()
+        th.join()
+    assert busy["resident"] and busy["jobs"] > 100
     assert sorted(lat)[len(lat) // 2] < 0.002, lat
     assert float(y.sum()) == 2 * (1 << 20)
-    kmws.handle_data_mask(b"\x01\x02\x03\x04", [bytearray(4096)])
-    t0 = time.perf_counter()
-    torch.cuda.synchronize()
-    assert time.perf_counter() - t0 < 0.05
 
 
 @pytest.mark.parametrize("n", [1, 3, 15, 16, 17, 1024, 4096, 65536, 65537, 300000, (1 << 20) + 5])
