@@ -953,7 +953,8 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v)
 #define KMWS_PACK_ROWS_PIPE 1  // two units in flight per wave (0: one; A/B builds)
 #endif
 
-// Small-frame batches (pack_rows_kernel): the prologue and the copy of one
+// Small-frame batches, a measured and rejected design (tuning builds only,
+// KMWS_PACK_ROWS_MAX_MEAN): the prologue and the copy of one
 // 256-frame row in ONE block.  The row's unit geometry and edge words stay in
 // LDS and the block's own waves copy the row's units (wave w takes slots w,
 // w + 4, ...; a frame cursor per wave, no search), so the edge-word buffer
@@ -962,7 +963,11 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v)
 // boundary between the two, and a row's boundary source lines are read by one
 // CU.  Load balance is a row's: batches of large frames keep the two-kernel
 // form (launch_copy_tail).  A bad batch (output over cap) stores nothing:
-// every block sees the same total before its first store.
+// every block sees the same total before its first store.  Measured on cfg4
+// (4 M x 4 KiB): HBM traffic 1.028 x algorithmic (the two-kernel form: 1.057
+// x) but 0.64 of peak against 0.72 -- 34 KiB of LDS per block holds 4 blocks
+// (16 waves) per CU against the copy grid's 32 waves, and a row's 512 units
+// are four waves' serial work; two units in flight per wave did not change it.
 template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                            const kmws_desc* __restrict__ d,
@@ -1469,22 +1474,26 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
     return launch_copy_tail<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
 }
 
-// The prologue and the copy grid, after the scan: one fused launch
-// (pack_rows_kernel) when the mean region is small -- cap / n bounds it from
-// above -- else the prologue and the copy grid.
+// The prologue and the copy grid, after the scan.  A tuning build
+// (KMWS_PACK_ROWS_MAX_MEAN = a mean-region bound in bytes; cap / n bounds the
+// mean from above) runs batches of small frames through the fused row kernel
+// instead: measured slower on cfg4 (0.64 vs 0.72 of HBM peak,
+// profiles/r04i_pack_rows_ab.txt), so the product never does.
 #ifndef KMWS_PACK_ROWS_MAX_MEAN
-#define KMWS_PACK_ROWS_MAX_MEAN 16384  // bytes; 0 = always the two-kernel form (A/B builds)
+#define KMWS_PACK_ROWS_MAX_MEAN 0
 #endif
 template <bool HEADERS>
 static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t nt = (uint32_t)n_tiles(n);
-    if (KMWS_PACK_ROWS_MAX_MEAN > 0 && cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
+#if KMWS_PACK_ROWS_MAX_MEAN > 0
+    if (cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
         hipLaunchKernelGGL(pack_rows_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, dst, d, flags,
                            n, cap, c.head, c.tiles, nt, c.grp, start);
         return hip_status(hipGetLastError());
     }
+#endif
     hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
                        c.head, c.tiles, nt, c.grp, start, c.rec, c.edge);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer

@@ -30,7 +30,8 @@
 //
 // usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [noresident]
 // (noresident: both loop threads switch their resident worker off -- every GPU
-// job a launch and a wait, the A/B of kmws_resident.hip)
+// job a launch and a wait, the A/B of kmws_resident.hip; submitpoll: the gpu
+// mode's flushes replaced by submit + poll(wait))
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -156,6 +157,7 @@ struct LoopObjs {
 // One connection: returns seconds from the first send to the last delivered frame.
 bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
 bool g_noresident = false;
+bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flushes
 
 double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
@@ -229,7 +231,11 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                     e.got.load() + kmws_rx_batch_pending(b) < kFrames)
                     continue;
                 const double tf = now_s();
-                if (kmws_rx_batch_flush(b) < 0) std::exit(5);
+                if (g_submitpoll) {  // the asynchronous pair, waited at once
+                    if (kmws_rx_batch_submit(b) < 0 || kmws_rx_batch_poll(b, 1) < 0) std::exit(5);
+                } else if (kmws_rx_batch_flush(b) < 0) {
+                    std::exit(5);
+                }
                 g_t.rx_flush += now_s() - tf;
                 pos = 0;  // ring bytes are free again after the flush
             }
@@ -399,7 +405,12 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             }
         }
         double tt = now_s();
-        if (gpu && !g_sync && kmws_tx_batch_flush(tx) != ng) std::exit(7);
+        if (gpu && !g_sync && g_submitpoll) {
+            const int64_t tk = kmws_tx_batch_submit(tx);
+            if (tk <= 0 || kmws_tx_batch_poll(tx, tk, 1) != 1) std::exit(7);
+        } else if (gpu && !g_sync && kmws_tx_batch_flush(tx) != ng) {
+            std::exit(7);
+        }
         g_t.tx_flush += now_s() - tt;
         iov.clear();
         for (int j = 0; j < ng; ++j) {
@@ -426,6 +437,7 @@ int main(int argc, char** argv)
     if (argc > 3) kGroup = std::max(1, std::atoi(argv[3]));
     if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
     g_noresident = argc > 5 && std::string(argv[5]) == "noresident";
+    g_submitpoll = argc > 5 && std::string(argv[5]) == "submitpoll";
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     const bool adapter = mode == "adapter";
     g_sync = mode == "sync";

@@ -92,9 +92,8 @@ def gpu_encode(T, src, offs, lens, flags, keys, cap=None):
 @pytest.mark.parametrize("aligned", [True, False])
 @pytest.mark.parametrize("room", [0, 20000])
 def test_encode_parity(T, kind, aligned, room):
-    """room = spare output capacity per frame: 0 takes the fused row kernel
-    (pack_rows_kernel) wherever the mean region is <= 16 KiB, 20000 forces the
-    prologue + copy-grid form (the kernel choice bounds the mean by cap / n)."""
+    """room = spare output capacity per frame (an output buffer larger than
+    the wire: nothing past the wire may be written)."""
     rng = np.random.default_rng(zlib.crc32(f"{kind}-{aligned}".encode()))
     n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6}[kind]
     lens, flags, keys = frames(rng, kind, n)
@@ -614,9 +613,9 @@ def test_batch_entries_empty_and_single(T, n):
 def test_encode_4k_frames_past_4_gib(T, room):
     """cfg4's shape (masked 4 KiB frames, 8-byte headers) at 1.1 M frames: the
     output crosses 2 GiB and 4 GiB (an offset with bit 31 set was once
-    sign-extended in the fused row kernel).  room 0: pack_rows_kernel; 20000:
-    the prologue + copy-grid form.  Every byte and offset checked on the
-    device against a torch restatement of encodeFrameHeader + mask."""
+    sign-extended in a tuning build's fused row kernel), with an exact and a
+    roomy output buffer.  Every byte and offset checked on the device against
+    a torch restatement of encodeFrameHeader + mask."""
     from kuma_amd import kmws
     n, L, H = (1 << 20) + (1 << 16), 4096, 8
     src = T.empty(n * L + 16, dtype=T.uint8, device="cuda")

@@ -98,16 +98,17 @@ def loopback(reps: int):
                                "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
                                "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", exe])
         for group in ("16", "64"):
-            for mode, extra in (("cpu", []), ("sync", []), ("gpu", []), ("gpu", ["0", "noresident"]), ("adapter", [])):
+            for mode, extra in (("cpu", []), ("sync", []), ("gpu", []), ("gpu", ["0", "noresident"]),
+                                ("gpu", ["0", "submitpoll"]), ("adapter", [])):
                 r = subprocess.run([exe, mode, str(reps), group] + extra, capture_output=True, text=True, timeout=300)
                 got = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
                 for x in got:
-                    x["resident"] = not extra
+                    x["variant"] = extra[1] if extra else ""
                 rows += got
     out = {"config": "loopback_cfg1", "rows": rows}
     for x in rows:
         out.setdefault("GiB_s", {}).setdefault(str(x.get("frames_per_send_iteration")), {})[
-            x["mode"] + ("" if x["resident"] else "_noresident")] = x.get("GiB_s")
+            x["mode"] + ("_" + x["variant"] if x["variant"] else "")] = x.get("GiB_s")
     return out
 
 
