@@ -137,6 +137,24 @@ def test_fuzz_encode_unpack_gather(T):
         assert int(out_err.max()) == 0 and ws_u.status() == 0 and ws_g.status() == 0
         orig = b"".join(bytes(src[int(o):int(o) + int(L)]) for o, L in zip(offs, lens))
         assert bytes(dst.cpu().numpy()[:len(orig)]) == orig, "gathered payloads differ"
+        # the fused forms: parse in the gather's scan; parse + plan, then unmask in place
+        fd = T.zeros((n, 2), dtype=T.int64, device="cuda")
+        fe = T.full((n,), 99, dtype=T.uint8, device="cuda")
+        dst2 = T.zeros(dst.numel(), dtype=T.uint8, device="cuda")
+        doff2 = T.zeros(n + 1, dtype=T.int64, device="cuda")
+        kmws.unpack_gather(wire, wire_off[:n], kmws.SERVER, fd, None, fe, dst2, doff2, ws_g, wire_len=total)
+        T.cuda.synchronize()
+        assert ws_g.status() == 0 and T.equal(fd, out_desc) and T.equal(fe, out_err) and T.equal(doff2, dst_off)
+        assert T.equal(dst2, dst), "fused gather differs"
+        w2 = wire.clone()
+        ws_m = kmws.Workspace(kmws.unmask_workspace_size(total))
+        kmws.unpack_unmask(w2, wire_off[:n], kmws.SERVER, fd, None, fe, ws_m, wire_len=total)
+        T.cuda.synchronize()
+        assert ws_m.status() == 0 and T.equal(fd, out_desc)
+        w2h = w2.cpu().numpy()
+        dd = out_desc.cpu().numpy().view(orc.DESC_DTYPE).reshape(-1)
+        assert b"".join(bytes(w2h[int(o):int(o) + int(L)]) for o, L in zip(dd["off"], dd["len"])) == orig, \
+            "fused in-place decode differs"
         # header-only pack: each 16-B slot is the wire image's header, zero-padded
         hdr = T.zeros(16 * n, dtype=T.uint8, device="cuda")
         hl = T.zeros(n, dtype=T.uint8, device="cuda")
