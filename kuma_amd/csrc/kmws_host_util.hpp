@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -157,12 +158,27 @@ public:
         (void)hipGetLastError();
         return true;  // finished, or failed: wait() reports which
     }
+    // Spins on the event for up to kSpinWaitUs first: hipEventSynchronize
+    // parks the thread, and waking it costs more than a small job (measured on
+    // the loopback cfg1 flush: 1.0 GiB/s parked vs 2.2 polled).  Longer jobs
+    // then park.
     kmws_status wait()
     {
         if (!launched_) return KMWS_OK;
         launched_ = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = hipEventQuery(done_);
+            if (e == hipSuccess) return KMWS_OK;
+            if (e != hipErrorNotReady) {
+                (void)hipGetLastError();
+                return KMWS_ERR_FAILED;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinWaitUs)) break;
+        }
         return hipEventSynchronize(done_) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
     }
+    static constexpr int kSpinWaitUs = 2000;
 
     // Enqueue the unmask of every staged descriptor (and `extra`) without waiting.
     kmws_status launch(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,

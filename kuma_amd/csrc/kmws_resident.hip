@@ -16,11 +16,14 @@
 // makes its stores visible system-wide and writes the job number back; the
 // host spins on that word.  No launch, no completion signal, no interrupt.
 //
-// The worker exits by itself after kResIdleUs (200 us) without a job (and on quit):
+// The worker exits by itself after kResIdleUs (200 us) without a job, after a
+// lease of kResLeaseUs (1 ms) however busy it is, and on quit:
 // every wave reaches the exit, the grid drains, and a host thread that stops
 // feeding never leaves a kernel behind.  The next job relaunches it.  It runs
-// on a non-blocking stream of its own, so work on other streams -- the legacy
-// default stream included -- does not queue behind it (tests/test_gpu_decoder.py).
+// on a non-blocking stream of its own at the greatest priority, so work on
+// other streams -- the legacy default stream included -- does not queue behind
+// it, and the lease bounds the wait of any kernel that still shares its
+// hardware queue (tests/test_gpu_decoder.py).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -50,6 +53,16 @@ constexpr int kResWords = 4;
 #define KMWS_RESIDENT_IDLE_US 200
 #endif
 constexpr uint32_t kResIdleUs = KMWS_RESIDENT_IDLE_US;
+// Lease: an incarnation also leaves after kResLeaseUs of life however busy it
+// is, before it takes the next job (the host relaunches it for that job).  A
+// thread that feeds back to back would otherwise keep the worker resident for
+// good, and a kernel on another stream that shares its hardware queue would
+// wait for as long (measured: up to 6.9 s behind a feeder thread).  The
+// relaunch it costs (~10-15 us) is spread over the ~100 jobs of one lease.
+#ifndef KMWS_RESIDENT_LEASE_US
+#define KMWS_RESIDENT_LEASE_US 1000
+#endif
+constexpr uint32_t kResLeaseUs = KMWS_RESIDENT_LEASE_US;
 
 static inline void cpu_relax()
 {
@@ -90,17 +103,19 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
 // One block, persistent until idle.  `last` = the job number already done when
 // it starts (jobs are numbered from 1); `inc` = this incarnation's number.
 __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* mb, uint64_t last, uint64_t inc,
-                                                                    uint64_t idle_ticks)
+                                                                    uint64_t idle_ticks, uint64_t lease_ticks)
 {
     __shared__ ResDesc s_d[kResMaxDescs];
     __shared__ uint32_t s_pre[kResMaxDescs + 1];  // word prefix over the payload hulls
     __shared__ uint64_t s_cmd;
     const int t = threadIdx.x;
+    const uint64_t born = wall_clock64();
     for (;;) {
         if (t == 0) {
             uint64_t cmd = 0;
             const uint64_t t0 = wall_clock64();
             for (;;) {
+                if ((uint64_t)(wall_clock64() - born) > lease_ticks) break;  // a posted job waits for the relaunch
                 const uint64_t w = ld_sys(&mb->word);
                 if (w & kQuitBit) break;
                 if ((w & kJobMask) != last) {
@@ -236,7 +251,7 @@ public:
             cpu_relax();
             if ((spin & 255) != 255) continue;
             if (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) == inc_) {
-                // idle exit raced with this job: done is written before exited
+                // idle or lease exit raced with this job: done is written before exited
                 if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
                 kmws_status st = launch((s - 1) & kJobMask);  // the new incarnation takes job s
                 if (st != KMWS_OK) return st;
@@ -279,8 +294,16 @@ private:
         // unless the caller picked another) waits for every blocking stream's
         // work, which would include this kernel -- measured: a kernel on the null
         // stream behind a CU-masked (blocking) worker stream waited out its idle
-        // time, 5.02 ms each time.
-        if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        // time, 5.02 ms each time.  At the greatest priority: the runtime keeps
+        // separate hardware queues per priority, so the worker does not share a
+        // queue with the process's ordinary streams unless those ask for the
+        // same priority (the lease bounds the wait when they do).
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+            (void)hipGetLastError();
+            greatest = least = 0;
+        }
+        if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest) != hipSuccess) {
             (void)hipGetLastError();
             return KMWS_ERR_FAILED;
         }
@@ -288,6 +311,7 @@ private:
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0)
             khz = 100000;  // gfx9 constant clock: 100 MHz
         idle_ticks_ = (uint64_t)khz * kResIdleUs / 1000u;
+        lease_ticks_ = (uint64_t)khz * kResLeaseUs / 1000u;
         // registered after the HIP runtime initialised (the calls above), so at
         // exit it runs before the runtime's own teardown
         static std::once_flag once;
@@ -300,7 +324,7 @@ private:
         DevGuard g(device_);
         ++inc_;
         hipLaunchKernelGGL(resident_unmask_kernel, dim3(1), dim3(kResBlock), 0, stream_, dmb_, last, inc_,
-                           idle_ticks_);
+                           idle_ticks_, lease_ticks_);
         if (hipGetLastError() != hipSuccess) {
             state_ = -1;
             return KMWS_ERR_FAILED;
@@ -316,7 +340,7 @@ private:
     ResMailbox* mb_ = nullptr;
     ResMailbox* dmb_ = nullptr;
     hipStream_t stream_ = nullptr;
-    uint64_t idle_ticks_ = 0;
+    uint64_t idle_ticks_ = 0, lease_ticks_ = 0;
     uint64_t seq_ = 0, inc_ = 0, jobs_ = 0;
 };
 
