@@ -927,7 +927,9 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     const uint64_t total = tot->a;
     // no early exit between these loads and their uses (the compiler would sink
     // the record load below the count's wait): an out-of-range wave owns no words
-    const UnitInfo x = decode_unit(r, u < total_units && st == 0, src);
+    // a bad header (fused decode) leaves the other frames to copy; a bad descriptor
+    // or an output past cap stops every store
+    const UnitInfo x = decode_unit(r, u < total_units && (st & kStatusBadDesc) == 0, src);
     // keep every field's load above the exit (one wait for all of them)
     asm volatile("" ::"s"(r.dst), "s"(r.src), "s"(r.f), "s"(r.rk), "s"(r.inner), "s"(total));
     if (x.khi == 0) return;  // wave-uniform, after the record's wait
