@@ -789,6 +789,12 @@ __device__ __forceinline__ UnitInfo decode_unit(const UnitRec& r, bool live, con
     return x;
 }
 
+// Source loads of the copy waves: non-temporal (streaming) by default.  A
+// shifted source run of 1 KiB per wave instruction starts mid-line, so two
+// instructions (or two waves) share its edge lines.
+#ifndef KMWS_COPY_NT_LOAD
+#define KMWS_COPY_NT_LOAD 1
+#endif
 constexpr int kUnitW = kUnitWords / 64;  // words per lane
 struct UnitRegs {
     u32x4 lo[kUnitW];  // aligned source word of each of the lane's output words
@@ -816,7 +822,11 @@ __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const ui
     for (int i = 0; i < kUnitW; ++i) {
         const uint32_t k = lane + 64 * i;
         const uint32_t kk = k < lo_k ? lo_k : (k < hi_k ? k : hi_k);
+#if KMWS_COPY_NT_LOAD
         R.lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * kk));
+#else
+        R.lo[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * kk);
+#endif
     }
     // word last + 1 holds payload bytes only when the source is shifted (delta != 0)
     uint32_t xk = x.fast && x.delta ? x.last + 1 : hi_k;
