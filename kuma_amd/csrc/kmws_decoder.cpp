@@ -57,6 +57,11 @@ struct kmws_decoder {
     int mode = KMWS_MODE_CLIENT;
     int device = 0;
     bool in_place = true;  // kmws_decoder_set_in_place
+    // The last chunk base found pageable: kuma reads into the same buffer every
+    // time (TcpConnection.cpp:229), and hipPointerGetAttributes per feed costs
+    // more than a small read's unmask.  Only that verdict is remembered: memory
+    // pinned since then is still staged (correct, slower), never the reverse.
+    const uint8_t* last_pageable = nullptr;
     // DecodeContext (WSHandler.h:66-78)
     kmws_frame_hdr hdr{};
     St state = St::HDR1;
@@ -100,6 +105,7 @@ struct kmws_rx_batch {
     std::vector<std::unique_ptr<PinnedStage>> spare;
     std::vector<Item>* delivering = nullptr;  // the generation whose callbacks are running
     uint8_t* ring = nullptr;  // caller's pinned receive ring (optional)
+    uint8_t* ring_dv = nullptr;  // its device view, looked up once at attach
     size_t ring_bytes = 0;
     int device = 0;
     bool flushing = false;  // feeding / submitting / polling from inside a delivery is refused
@@ -319,6 +325,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     dec->chunk_descs.clear();
     dec->stage.clear();
     int chunk_pinned = -1;  // resolved at the first masked in-chunk frame
+    uint8_t* chunk_dv = nullptr;
     uint8_t* chunk_base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(data) & ~(uintptr_t)15);
 
     auto sink = [&](const kmws_frame_hdr& h, uint8_t* payload, std::vector<uint8_t>* reasm) -> int {
@@ -336,7 +343,12 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
             if (!masked) {
                 q.where = kInChunk;
             } else {
-                if (chunk_pinned < 0) chunk_pinned = device_view(chunk_base) != nullptr;
+                if (chunk_pinned < 0) {
+                    chunk_dv = chunk_base == dec->last_pageable ? nullptr
+                                                                : static_cast<uint8_t*>(device_view(chunk_base));
+                    chunk_pinned = chunk_dv != nullptr;
+                    if (!chunk_pinned) dec->last_pageable = chunk_base;
+                }
                 if (chunk_pinned) {
                     dec->chunk_descs.push_back(kmws_desc{(uint64_t)(payload - chunk_base), h.length, key});
                     q.where = kInChunkPinned;
@@ -370,7 +382,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     // ---- GPU unmask of every masked payload of this call ----
     if (dec->stage.n_desc() || !dec->chunk_descs.empty()) {
         const uint64_t chunk_span = (uint64_t)((data + len) - chunk_base);
-        kmws_status st = dec->stage.run(chunk_base, chunk_span, &dec->chunk_descs);
+        kmws_status st = dec->stage.run(chunk_base, chunk_span, &dec->chunk_descs, chunk_dv);
         if (st != KMWS_OK) return st;
     }
 
@@ -512,6 +524,7 @@ struct kmws_tx_batch {
     size_t bytes = 0;
     int device = 0;
     uint8_t* ring = nullptr;  // caller's pinned send ring (optional)
+    uint8_t* ring_dv = nullptr;  // its device view, looked up once at attach
     size_t ring_bytes = 0;
     std::vector<kmws_desc> ring_descs;
     std::deque<Gen> inflight;
@@ -592,8 +605,10 @@ kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ri
     if (!b || (ring && !ring_bytes)) return KMWS_ERR_INVALID_PARAM;
     // queued segments were classified already; a mask in flight may still be writing into the old ring
     if (!b->frames.empty() || !b->inflight.empty()) return KMWS_ERR_INVALID_STATE;
-    if (ring && !device_view(ring)) return KMWS_ERR_INVALID_PARAM;  // must be pinned
+    uint8_t* dv = ring ? static_cast<uint8_t*>(device_view(ring)) : nullptr;
+    if (ring && !dv) return KMWS_ERR_INVALID_PARAM;  // must be pinned
     b->ring = ring;
+    b->ring_dv = dv;
     b->ring_bytes = ring ? ring_bytes : 0;
     return KMWS_OK;
 }
@@ -635,9 +650,9 @@ static int64_t tx_submit(kmws_tx_batch* b, bool sync)
             }
         }
         if (sync)
-            st = b->ring_descs.empty() ? s.run() : s.run(b->ring, b->ring_bytes, &b->ring_descs);
+            st = b->ring_descs.empty() ? s.run() : s.run(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv);
         else
-            st = b->ring_descs.empty() ? s.launch() : s.launch(b->ring, b->ring_bytes, &b->ring_descs);
+            st = b->ring_descs.empty() ? s.launch() : s.launch(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv);
     }
     b->frames.clear();
     b->ring_descs.clear();
@@ -756,8 +771,10 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
 kmws_status kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t bytes)
 {
     if (!b || b->flushing || !b->items.empty() || !b->inflight.empty()) return KMWS_ERR_INVALID_STATE;
-    if (ring && (!bytes || !device_view(ring))) return KMWS_ERR_INVALID_PARAM;  // must be pinned
+    uint8_t* dv = ring && bytes ? static_cast<uint8_t*>(device_view(ring)) : nullptr;
+    if (ring && !dv) return KMWS_ERR_INVALID_PARAM;  // must be pinned
     b->ring = ring;
+    b->ring_dv = dv;
     b->ring_bytes = ring ? bytes : 0;
     return KMWS_OK;
 }
@@ -788,8 +805,8 @@ static int rx_submit(kmws_rx_batch* b, bool sync)
     if (b->items.empty()) return 0;
     std::unique_ptr<PinnedStage> next = b->take_stage();
     if (!next) return KMWS_ERR_FAILED;
-    kmws_status st = sync ? b->stage->run(b->ring, b->ring_bytes, &b->ring_descs)
-                          : b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs);
+    kmws_status st = sync ? b->stage->run(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv)
+                          : b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv);
     b->ring_descs.clear();
     if (st != KMWS_OK) {
         // nothing of this generation can be delivered masked: drop it

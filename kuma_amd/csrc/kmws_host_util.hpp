@@ -129,22 +129,25 @@ public:
     // pinned memory: no plan kernels, no copies, no status read-back.
     // Small jobs go to this thread's resident worker (no launch, no event wait;
     // kmws_resident.hip); larger ones are launched on the stage's stream.
+    // extra_dv: the device view of extra_base if the caller has it (a ring
+    // attached once); else it is looked up here (hipPointerGetAttributes).
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
-                    const std::vector<kmws_desc>* extra = nullptr)
+                    const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
     {
         const size_t n2 = extra ? extra->size() : 0;
+        if (n2 && !extra_dv) extra_dv = static_cast<uint8_t*>(device_view(extra_base));
         if (descs_.size() + n2 <= (size_t)kResMaxDescs && descs_.size() + n2 > 0) {
             bool ok = true;
             for (size_t i = 0; i < n2; ++i) ok &= (*extra)[i].off + (*extra)[i].len <= extra_span;
             if (!ok) return KMWS_ERR_INVALID_PARAM;
-            const uint8_t* dv2 = n2 ? static_cast<const uint8_t*>(device_view(extra_base)) : nullptr;
+            const uint8_t* dv2 = n2 ? extra_dv : nullptr;
             if (n2 && !dv2) return KMWS_ERR_INVALID_PARAM;
             if (descs_.size() && !dv_h_) return KMWS_ERR_FAILED;
             const kmws_status st = resident_unmask(device_, descs_.data(), dv_h_, descs_.size(),
                                                    n2 ? extra->data() : nullptr, dv2, n2);
             if (st != KMWS_ERR_NOT_SUPPORTED) return st;
         }
-        kmws_status st = launch(extra_base, extra_span, extra);
+        kmws_status st = launch(extra_base, extra_span, extra, extra_dv);
         if (st != KMWS_OK) return st;
         return wait();
     }
@@ -182,7 +185,7 @@ public:
 
     // Enqueue the unmask of every staged descriptor (and `extra`) without waiting.
     kmws_status launch(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
-                       const std::vector<kmws_desc>* extra = nullptr)
+                       const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
     {
         const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
         if (n1 + n2 == 0) return KMWS_OK;
@@ -219,8 +222,9 @@ public:
             if (st != KMWS_OK) return st;
         }
         if (p2) {
-            uint8_t* dv = static_cast<uint8_t*>(device_view(eb));
-            if (!dv) return KMWS_ERR_INVALID_PARAM;
+            if (!extra_dv) extra_dv = static_cast<uint8_t*>(device_view(extra_base));
+            if (!extra_dv) return KMWS_ERR_INVALID_PARAM;
+            uint8_t* dv = extra_dv - delta;  // the aligned base's view (one mapping per allocation)
             st = launch_unmask_pieces(dv, dv_desc_ + n1, dv_piece_ + p1, (uint32_t)p2, stream_);
             if (st != KMWS_OK) return st;
         }

@@ -961,6 +961,331 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v)
     return (uint64_t)hi << 32 | lo;
 }
 
+__device__ __forceinline__ u32x4 shfl16_down1(const u32x4& v)
+{
+    return u32x4{(uint32_t)__shfl_down((int)v.x, 1, 64), (uint32_t)__shfl_down((int)v.y, 1, 64),
+                 (uint32_t)__shfl_down((int)v.z, 1, 64), (uint32_t)__shfl_down((int)v.w, 1, 64)};
+}
+
+// ------------------------------ chunk copy ------------------------------
+// The product form of encode and gather: output-stationary.  The output is cut
+// into 4 KiB chunks on 4 KiB boundaries, one wave each, so every output line is
+// written by one store instruction of one wave, and nothing per frame or per
+// wave passes through memory between the kernels but the region offsets and
+// one 4-byte entry per chunk (the frame holding its first byte).  A chunk's
+// frames -- up to 64, one lane each -- go into a wave-private table in LDS;
+// each of its words finds its frame there and is either an interior word
+// (inside one payload: two aligned source words, funnel-shifted and XORed with
+// the rotated key) or a boundary word (header bytes, a payload's end, the next
+// frame's start).  Boundary words are listed per wave and composed byte-parallel
+// (one lane per byte), from source lines the same wave reads for its interior
+// words anyway -- round 3's prologue read them in a pass of its own (0.97 GiB
+// more fetched on cfg4) and wrote 80 B of edge words and two
+// 32 B unit records per 4 KiB frame; here their values join the chunk's four
+// full-width stores through LDS.
+constexpr uint64_t kChunkBytes = 4096;
+constexpr uint32_t kChunkWords = (uint32_t)(kChunkBytes / 16);
+constexpr uint32_t kChunkW = kChunkWords / 64;  // words per lane
+constexpr uint32_t kChunkFrames = 64;           // a chunk's frame table, one lane per frame
+
+__host__ __device__ __forceinline__ uint64_t chunk_count(uint64_t bytes) { return (bytes + kChunkBytes - 1) / kChunkBytes; }
+
+// 256 frames per block, after the scan: each frame's region offset (start[f])
+// and, for every chunk whose first byte lies in the block's regions, the frame
+// holding it (cmap[c]).  Also the capacity check (status set, nothing stored).
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) chunk_map_kernel(const kmws_desc* __restrict__ d,
+                                                           const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
+                                                           WsHead* __restrict__ head, const V2* __restrict__ tiles,
+                                                           uint32_t ntiles, const V2* __restrict__ grp,
+                                                           uint64_t* __restrict__ start, uint32_t* __restrict__ cmap)
+{
+    __shared__ uint64_t s_r0[kBlock + 1];
+    __shared__ V2 s_w[kBlock / 64];
+    const uint32_t t = threadIdx.x;
+    const uint64_t F0 = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
+    const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
+    const V2 tot = tiles[ntiles];
+    const V2 pre = tiles[blockIdx.x / kRowsPerTile] + grp[blockIdx.x];
+    const kmws_desc x = d[f];
+    const uint32_t fl = HEADERS ? flags[f] : 0u;
+    const uint64_t rsz = (uint64_t)(HEADERS ? hdr_len(x.len, (fl >> 8) & 1u) : 0u) + x.len;
+    if (blockIdx.x == 0 && t == 0) head->pad[0] = 0;  // chunk_copy_kernel's dense-chunk count
+    V2 row;
+    const V2 off = block_excl_scan(t < nf ? V2{rsz, 0} : V2{0, 0}, s_w, row);
+    const uint64_t r0 = pre.a + off.a;
+    if (t < nf) {
+        start[f] = r0;
+        s_r0[t] = r0;
+    }
+    if (t == 0) s_r0[nf] = pre.a + row.a;
+    if (tot.a > cap) {  // block-uniform; the copy waves see the status and store nothing
+        if (blockIdx.x == 0 && t == 0) atomicOr(&head->status, kStatusBadDesc);
+        return;
+    }
+    __syncthreads();
+    const uint64_t c0 = chunk_count(pre.a), c1 = chunk_count(pre.a + row.a);
+    for (uint64_t c = c0 + t; c < c1; c += kBlock) {
+        const uint64_t xb = c * kChunkBytes;
+        uint32_t lo = 0, hi = nf;  // s_r0[lo] <= xb < s_r0[hi]: the last region starting at or before xb
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_r0[mid] <= xb) lo = mid; else hi = mid;
+        }
+        cmap[c] = (uint32_t)F0 + lo;
+    }
+}
+
+struct ChunkFrame {  // one frame of a chunk's table (LDS), 32 B
+    uint64_t r0;     // region start in the output
+    uint64_t sdel;   // source byte - output byte over the payload (mod 2^64)
+    uint32_t len;
+    uint32_t key;    // key to apply (0 = none)
+    uint32_t hl;     // header bytes
+    uint32_t fl;     // flags (encode)
+};
+
+// LDS written by some lanes of a wave and read by others: DS instructions of
+// one wave execute in order; this keeps the compiler from reordering them.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t bal)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+// The output's last, partial word: bytes [a, total) only.
+__device__ __forceinline__ void store_word_bytes(uint8_t* __restrict__ dst, uint64_t a, uint64_t total, const u32x4& v)
+{
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (uint64_t p = a; p < total; ++p) {
+        const uint32_t b = (uint32_t)(p - a);
+        const uint32_t w = (b & 8u) ? ((b & 4u) ? v.w : v.z) : ((b & 4u) ? v.y : v.x);
+        dst[p] = (uint8_t)(w >> (8 * (b & 3u)));
+    }
+}
+
+__device__ __forceinline__ u32x4 copy_src_load(const uint8_t* p)
+{
+#if KMWS_COPY_NT_LOAD
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+    return *reinterpret_cast<const u32x4*>(p);
+#endif
+}
+
+// Output byte x of frame e (x inside its region): a header byte
+// (WSHandler::encodeFrameHeader) or a masked payload byte.
+template <bool HEADERS>
+__device__ __forceinline__ uint32_t chunk_byte(const ChunkFrame& e, uint64_t x, const uint8_t* __restrict__ src)
+{
+    const uint64_t p0 = e.r0 + e.hl;
+    if (HEADERS && x < p0) {
+        uint64_t h0, h1;
+        build_header(e.len, e.fl, e.key, h0, h1);
+        const uint32_t k = (uint32_t)(x - e.r0);
+        return (uint32_t)((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8))) & 0xFFu);
+    }
+    return src[x + e.sdel] ^ ((e.key >> (8 * ((x - p0) & 3u))) & 0xFFu);
+}
+
+// One wave per 4 KiB output chunk (4 words per lane, 1 KiB per instruction).
+// A chunk meeting more than kChunkFrames frames is listed for chunk_dense_kernel.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                            const kmws_desc* __restrict__ d,
+                                                            const uint16_t* __restrict__ flags, uint32_t n,
+                                                            const uint64_t* __restrict__ start,
+                                                            const uint32_t* __restrict__ cmap,
+                                                            const V2* __restrict__ tot, WsHead* __restrict__ head,
+                                                            uint32_t* __restrict__ dense, uint64_t chunk_base,
+                                                            uint32_t split)
+{
+    __shared__ ChunkFrame s_tab[kBlock / 64][kChunkFrames];
+    __shared__ uint32_t s_slow[kBlock / 64][kChunkWords];
+    __shared__ u32x4 s_val[kBlock / 64][64 + 4];  // boundary words 0..63, then 4 scratch slots
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // consecutive blocks dealt over `split` parts of the output: with split 8,
+    // XCD x (blocks are dispatched round-robin over the 8 XCDs) streams part x
+    uint32_t b = blockIdx.x;
+    const uint32_t q = gridDim.x / split;
+    if (b < q * split) b = (b % split) * q + b / split;
+    const uint64_t c = chunk_base + (uint64_t)b * (kBlock / 64) + wave;
+    const uint64_t total = tot->a;
+    const uint32_t st = head->status;
+    const uint64_t nch = chunk_count(total);
+    if (c >= nch || (st & kStatusBadDesc)) return;  // wave-uniform
+    const uint32_t f0 = cmap[c];
+    const uint32_t f1 = c + 1 < nch ? cmap[c + 1] : n - 1;  // holds the next chunk's first byte
+    const uint32_t nfr = f1 - f0 + 1;
+    const uint64_t A0 = c * kChunkBytes;
+    if (nfr > kChunkFrames) {
+        if (lane == 0) dense[atomicAdd(&head->pad[0], 1u)] = (uint32_t)c;
+        return;
+    }
+    ChunkFrame* tab = s_tab[wave];
+    if ((uint32_t)lane < nfr) {
+        const uint32_t j = f0 + lane;
+        const kmws_desc x = d[j];
+        const uint32_t fl = HEADERS ? flags[j] : 0u;
+        const uint32_t mask = HEADERS ? (fl >> 8) & 1u : 1u;
+        ChunkFrame e;
+        e.r0 = start[j];
+        e.hl = HEADERS ? hdr_len(x.len, mask) : 0u;
+        e.sdel = x.off - (e.r0 + e.hl);
+        e.len = x.len;
+        e.key = mask ? x.key : 0u;
+        e.fl = fl;
+        tab[lane] = e;
+    }
+    wave_lds_sync();
+    // Pass 1: each word's frame (binary search over the table) and kind.  An
+    // interior word lies inside one payload; it takes its second source word
+    // from the next word's lane (lane 63: lane 0 of the next round) when that
+    // word is interior to the same payload.  Every other live word -- header
+    // bytes, a payload's first or last bytes, the last interior word before a
+    // boundary, the chunk's last word -- is listed as a boundary word.
+    uint32_t* sl = s_slow[wave];
+    uint32_t jbits = 0, slowbits = 0, nslow = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kChunkW; ++i) {
+        const uint32_t k = 64u * i + lane;
+        const uint64_t a = A0 + 16ull * k;
+        uint32_t lo = 0, hi = nfr;  // tab[lo].r0 <= a < tab[hi].r0
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab[mid].r0 <= a) lo = mid; else hi = mid;
+        }
+        const ChunkFrame e = tab[lo];
+        const uint64_t p0 = e.r0 + e.hl, r1 = p0 + e.len;
+        const bool live = a < total;
+        const bool inner = live && a >= p0 && a + 16 <= r1;
+        const uint32_t delta = (uint32_t)((a + e.sdel) & 15u);
+        const bool fast = inner && (delta == 0 || (a + 32 <= r1 && (i + 1 < (int)kChunkW || lane != 63)));
+        const bool slow = live && !fast;
+        const uint64_t bal = __ballot(slow);
+        if (slow) sl[nslow + lanes_below(bal)] = k | lo << 16;
+        jbits |= lo << (6 * i);
+        slowbits |= slow ? 1u << i : 0u;
+        nslow += (uint32_t)__builtin_popcountll(bal);
+    }
+    wave_lds_sync();
+    // Pass 2: interior words' source words, one aligned word each (all four
+    // rounds issued before anything waits).
+    u32x4 L0[kChunkW];
+    uint32_t rk[kChunkW], dl = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kChunkW; ++i) {
+        const uint64_t a = A0 + 16ull * (64u * i + lane);
+        const ChunkFrame e = tab[(jbits >> (6 * i)) & 63u];
+        const uint64_t p0 = e.r0 + e.hl, r1 = p0 + e.len;
+        const bool inner = a < total && a >= p0 && a + 16 <= r1;
+        const uint64_t sa = a + e.sdel;
+        L0[i] = copy_src_load(src + (inner ? sa & ~15ull : 0));
+        dl |= (uint32_t)(sa & 15u) << (4 * i);
+        rk[i] = e.key ? rot_key(e.key, p0) : 0u;
+    }
+    // Pass 3: boundary words, byte-parallel -- four words at a time, one lane
+    // per byte (its frame found from the word's first frame on; a header byte
+    // or a masked source byte), assembled in LDS.  The first 64 join the stores
+    // of pass 4; more (chunks of many small frames) are stored here.
+    uint8_t* sb = reinterpret_cast<uint8_t*>(&s_val[wave][0]);
+    for (uint32_t g0 = 0; g0 < nslow; g0 += 4) {  // wave-uniform
+        const uint32_t qi = g0 + ((uint32_t)lane >> 4), bi = lane & 15;
+        if (qi < nslow) {
+            const uint32_t ent = sl[qi];
+            uint32_t m = ent >> 16;
+            const uint64_t x = A0 + 16ull * (ent & 0xFFFFu) + bi;
+            while (m + 1 < nfr && tab[m + 1].r0 <= x) ++m;
+            const uint32_t v = x < total ? chunk_byte<HEADERS>(tab[m], x, src) : 0u;
+            sb[16u * (qi < 64 ? qi : 64 + ((uint32_t)lane >> 4)) + bi] = (uint8_t)v;
+        }
+        if (g0 >= 64) {  // wave-uniform: four words past the first 64, stored now
+            wave_lds_sync();
+            if (lane < 4 && g0 + lane < nslow) {
+                const uint64_t a = A0 + 16ull * (sl[g0 + lane] & 0xFFFFu);
+                const u32x4 v = s_val[wave][64 + lane];
+                if (a + 16 <= total) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + a));
+                else store_word_bytes(dst, a, total, v);
+            }
+            wave_lds_sync();  // the scratch slots are reused
+        }
+    }
+    wave_lds_sync();
+    // Pass 4: the four full-width stores, boundary words merged in.
+    uint32_t seen = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kChunkW; ++i) {
+        const uint32_t k = 64u * i + lane;
+        const uint64_t a = A0 + 16ull * k;
+        u32x4 hi = shfl16_down1(L0[i]);
+        if (i + 1 < (int)kChunkW) {
+            const u32x4 nx = readlane0(L0[i + 1 < (int)kChunkW ? i + 1 : i]);
+            if (lane == 63) hi = nx;
+        }
+        u32x4 out = funnel16(L0[i], hi, (dl >> (4 * i)) & 15u) ^ rk[i];
+        const bool slow = (slowbits >> i) & 1u;
+        const uint64_t bal = __ballot(slow);
+        bool mine = true;
+        if (bal) {  // wave-uniform
+            const uint32_t pos = seen + lanes_below(bal);
+            if (slow) {
+                mine = pos < 64;
+                if (mine) out = s_val[wave][pos];
+            }
+            seen += (uint32_t)__builtin_popcountll(bal);
+        }
+        if (mine && a + 16 <= total) __builtin_nontemporal_store(out, reinterpret_cast<u32x4*>(dst + a));
+        else if (mine && a < total) store_word_bytes(dst, a, total, out);
+    }
+}
+
+// The chunks chunk_copy_kernel listed (more than kChunkFrames frames: regions
+// averaging under 64 bytes): every word byte by byte, its first frame by a
+// binary search over start[].  Correct for any batch, fast only where it does
+// not matter; a batch of small frames takes the unit form instead (below).
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) chunk_dense_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                             const kmws_desc* __restrict__ d,
+                                                             const uint16_t* __restrict__ flags, uint32_t n,
+                                                             const uint64_t* __restrict__ start,
+                                                             const uint32_t* __restrict__ cmap,
+                                                             const V2* __restrict__ tot,
+                                                             const WsHead* __restrict__ head,
+                                                             const uint32_t* __restrict__ dense)
+{
+    if (head->status & kStatusBadDesc) return;
+    const uint32_t cnt = head->pad[0];
+    const uint64_t total = tot->a, nch = chunk_count(total);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * (kBlock / 64);
+    for (uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < cnt; i += nw) {
+        const uint64_t c = dense[i];
+        const uint32_t f0 = cmap[c], f1 = c + 1 < nch ? cmap[c + 1] : n - 1;
+        for (uint32_t k = lane; k < kChunkWords; k += 64) {
+            const uint64_t a = c * kChunkBytes + 16ull * k;
+            if (a >= total) break;
+            uint32_t lo = f0, hi = f1 + 1;  // start[lo] <= a < start[hi] (start[n] = total)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (start[mid] <= a) lo = mid; else hi = mid;
+            }
+            const uint32_t fl = HEADERS ? flags[lo] : 0u;
+            const FrameGeom g = geom_at<HEADERS>(d[lo], fl, start[lo]);
+            const u32x4 v = compose_word_bytes<HEADERS>(a, lo, n, src, g, fl, d, flags);
+            if (a + 16 <= total) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + a));
+            else store_word_bytes(dst, a, total, v);
+        }
+    }
+}
+
 #ifndef KMWS_PACK_ROWS_PIPE
 #define KMWS_PACK_ROWS_PIPE 1  // two units in flight per wave (0: one; A/B builds)
 #endif
@@ -1405,12 +1730,20 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 }
 
 // ------------------------------ host launchers ------------------------------
+// The copy form: chunk_map + chunk_copy (product), or the round-3 form --
+// prologue (edge words, unit records) + copy_kernel -- in a tuning build
+// (KMWS_PACK_UNITS=1) for A/B runs.
+#ifndef KMWS_PACK_UNITS
+#define KMWS_PACK_UNITS 0
+#endif
 struct CopyWs {
     WsHead* head;
     V2* tiles;  // ntiles + 1: tile prefixes, then the totals
     V2* grp;    // one per 256-frame row: its prefix inside the tile
     UnitRec* rec;
     u32x4* edge;
+    uint32_t* cmap;   // chunk -> frame holding its first byte
+    uint32_t* dense;  // chunks chunk_copy_kernel left to chunk_dense_kernel
 };
 
 static uint64_t n_tiles(uint32_t n) { return ((uint64_t)n + kScanTile - 1) / kScanTile; }
@@ -1440,7 +1773,12 @@ static void carve_scan(char* p, uint32_t n, CopyWs& c)
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
+#if KMWS_PACK_UNITS
     return r256(scan_ws_size(n)) + r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
+#else
+    return r256(scan_ws_size(n)) + r256((chunk_count(cap) + 1) * sizeof(uint32_t)) +
+           r256(chunk_count(cap) * sizeof(uint32_t));
+#endif
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -1448,8 +1786,10 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     if (!ws || ws_bytes < copy_ws_size(n, cap)) return false;
     char* p = static_cast<char*>(ws);
     carve_scan(p, n, c);
-    p += r256(scan_ws_size(n));  // edge words and records on whole lines
+    p += r256(scan_ws_size(n));  // edge words and records (or the chunk map) on whole lines
     c.edge = reinterpret_cast<u32x4*>(p);
+    c.cmap = reinterpret_cast<uint32_t*>(p);
+    c.dense = c.cmap + r256((chunk_count(cap) + 1) * sizeof(uint32_t)) / sizeof(uint32_t);
     p += r256((uint64_t)n * kEdgeWords * 16);
     c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
@@ -1499,6 +1839,25 @@ static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t c
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t nt = (uint32_t)n_tiles(n);
+#if !KMWS_PACK_UNITS
+    hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, d, flags, n, cap,
+                       c.head, c.tiles, nt, c.grp, start, c.cmap);
+    {
+        const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
+        constexpr uint64_t kWaves = kBlock / 64;
+        constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
+        for (uint64_t c0 = 0; c0 < chunks; c0 += kMaxChunksPerLaunch) {
+            const uint64_t nc = chunks - c0 < kMaxChunksPerLaunch ? chunks - c0 : kMaxChunksPerLaunch;
+            hipLaunchKernelGGL(chunk_copy_kernel<HEADERS>, dim3((uint32_t)((nc + kWaves - 1) / kWaves)), dim3(kBlock),
+                               0, s, src, dst, d, flags, n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0,
+                               kCopySplit);
+        }
+        const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
+        hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n,
+                           start, c.cmap, c.tiles + nt, c.head, c.dense);
+    }
+    return hip_status(hipGetLastError());
+#else
 #if KMWS_PACK_ROWS_MAX_MEAN > 0
     if (cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
         hipLaunchKernelGGL(pack_rows_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, dst, d, flags,
@@ -1522,6 +1881,7 @@ static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t c
                            dim3(kBlock), lds_pad, s, src, dst, c.tiles + nt, c.rec, c.edge, c.head, u0, kCopySplit);
     }
     return hip_status(hipGetLastError());
+#endif
 }
 
 }  // namespace kmws

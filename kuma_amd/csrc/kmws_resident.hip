@@ -79,16 +79,41 @@ struct ResDesc {  // one payload: device-visible address, bytes, LE key of its f
 static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 
 // Pinned host memory, polled by the worker.  Host-written and device-written
-// words sit in different 128-byte lines.  The polled word carries everything
-// the worker needs before it reads the descriptors, so a job costs one PCIe
-// round trip to notice and one to read its descriptors: job number (bits
-// 0-39), payload count (40-47) and the quit bit (63).
+// words sit in different 128-byte lines.  The polled word carries the job
+// number (bits 0-39), the payload count (40-47) and the quit bit (63); the
+// first kPollDescs descriptor slots follow it and are read with it at every
+// poll, so a job of up to kPollDescs payloads costs one PCIe round trip to
+// notice and none more to read its descriptors.  The host rewrites every one
+// of those slots for every job (unused ones with length 0), each half of a
+// slot tagged with the job's low bits (address bits 48-63, length bits
+// 21-31): a slot read before the host's write landed carries the previous
+// job's tag, and the job's descriptors are then read again after the word.
 constexpr uint64_t kJobMask = (1ull << 40) - 1;
 constexpr uint64_t kQuitBit = 1ull << 63;
+constexpr int kPollDescs = 15;  // word + 15 slots: the mailbox's first 256 bytes
+constexpr uint64_t kAddrMask = (1ull << 48) - 1;
+constexpr uint32_t kLenMask = (1u << 21) - 1;  // kResMaxBytes fits
+static_assert(kResMaxBytes <= kLenMask, "tagged length");
+__host__ __device__ __forceinline__ ResDesc tag_desc(ResDesc x, uint64_t job)
+{
+    x.addr |= (job & 0xFFFFull) << 48;
+    x.len |= (uint32_t)(job & 0x7FFu) << 21;
+    return x;
+}
+__host__ __device__ __forceinline__ bool desc_tagged(const ResDesc& x, uint64_t job)
+{
+    return (x.addr >> 48) == (job & 0xFFFFull) && (x.len >> 21) == (uint32_t)(job & 0x7FFu);
+}
+__host__ __device__ __forceinline__ ResDesc untag_desc(ResDesc x)
+{
+    x.addr &= kAddrMask;
+    x.len &= kLenMask;
+    return x;
+}
 struct alignas(256) ResMailbox {
     uint64_t word;  // job | ndesc << 40 | quit << 63, written last by the host (release)
-    uint64_t pad1[7];
-    ResDesc desc[kResMaxDescs];
+    uint64_t pad1;
+    ResDesc desc[kResMaxDescs];  // desc[i] at 16 + 16 i
     alignas(128) uint64_t done;    // job number finished (device, release: payloads visible)
     alignas(128) uint64_t exited;  // incarnation number of the worker that exited
     alignas(128) uint64_t pad2[16];
@@ -108,15 +133,24 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     __shared__ ResDesc s_d[kResMaxDescs];
     __shared__ uint32_t s_pre[kResMaxDescs + 1];  // word prefix over the payload hulls
     __shared__ uint64_t s_cmd;
+    __shared__ uint32_t s_have;  // descriptors taken from the poll
     const int t = threadIdx.x;
     const uint64_t born = wall_clock64();
+    // lane l <= kPollDescs of wave 0 polls bytes [16 l, 16 l + 16) of the
+    // mailbox: the job word (lane 0) and descriptor slot l - 1; the other
+    // lanes load lane 0's address (one request)
+    const uint64_t* pw = reinterpret_cast<const uint64_t*>(mb) + 2 * (t <= kPollDescs ? t : 0);
     for (;;) {
-        if (t == 0) {
-            uint64_t cmd = 0;
+        if (t < 64) {  // wave 0, uniform control flow
+            uint64_t cmd = 0, v0 = 0, v1 = 0;
             const uint64_t t0 = wall_clock64();
             for (;;) {
                 if ((uint64_t)(wall_clock64() - born) > lease_ticks) break;  // a posted job waits for the relaunch
-                const uint64_t w = ld_sys(&mb->word);
+                v0 = ld_sys(pw);
+                v1 = ld_sys(pw + 1);
+                const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32;
+                // (lane 0's job word; each half through uint32_t: readfirstlane is signed)
                 if (w & kQuitBit) break;
                 if ((w & kJobMask) != last) {
                     cmd = w;
@@ -125,18 +159,32 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 if ((uint64_t)(wall_clock64() - t0) > idle_ticks) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            // acquire at system scope (the CU's vector L1 and the L2): the
-            // descriptors and payloads the host wrote before the job word are
-            // read fresh; the other waves load after the barrier below
-            if (cmd) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            s_cmd = cmd;
+            uint32_t have = 0;
+            if (cmd) {
+                const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
+                const ResDesc x = ResDesc{v0, (uint32_t)v1, (uint32_t)(v1 >> 32)};
+                const bool mine = t >= 1 && t <= (int)nd && t <= kPollDescs;
+                const bool ok = desc_tagged(x, cmd & kJobMask);
+                if (mine && ok) s_d[t - 1] = untag_desc(x);
+                // every descriptor of the job came with the word: no second round trip
+                const uint64_t bad = __ballot(mine && !ok);
+                have = nd <= (uint32_t)kPollDescs && bad == 0 ? nd : 0u;
+                // acquire at system scope (the CU's vector L1 and the L2): the
+                // payloads (and descriptors) the host wrote before the job word
+                // are read fresh; the other waves load after the barrier below
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            }
+            if (t == 0) {
+                s_cmd = cmd;
+                s_have = have;
+            }
         }
         __syncthreads();
         const uint64_t cmd = s_cmd;
         if (cmd == 0) break;  // every wave leaves together
         const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
         const uint32_t n = nd < (uint32_t)kResMaxDescs ? nd : (uint32_t)kResMaxDescs;
-        if (t < (int)n) s_d[t] = mb->desc[t];
+        if (s_have == 0 && t < (int)n) s_d[t] = untag_desc(mb->desc[t]);
         __syncthreads();
         if (t == 0) {
             uint32_t w = 0;
@@ -242,8 +290,13 @@ public:
             kmws_status st = launch(seq_ & kJobMask);  // every earlier job is done
             if (st != KMWS_OK) return st;
         }
-        std::memcpy(mb_->desc, d, n * sizeof(ResDesc));
-        const uint64_t s = ++seq_ & kJobMask;
+        const uint64_t s = (seq_ + 1) & kJobMask;
+        for (uint32_t i = 0; i < n; ++i)
+            if ((d[i].addr >> 48) != 0 || d[i].len > kLenMask) return KMWS_ERR_NOT_SUPPORTED;
+        // every polled slot is rewritten, so a stale one always carries job s - 1's tag
+        for (uint32_t i = 0; i < n || i < (uint32_t)kPollDescs; ++i)
+            mb_->desc[i] = tag_desc(i < n ? d[i] : ResDesc{0, 0, 0}, s);
+        ++seq_;
         __atomic_store_n(&mb_->word, s | (uint64_t)n << 40, __ATOMIC_RELEASE);
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0;; ++spin) {

@@ -1,6 +1,6 @@
 """Times the copy kernels (encode / gather) of ONE build of the library, loaded
 alone (two builds in one process interfere): run it once per build in the same
-gpurun call and compare.  Usage: python tools/ab_pack.py <lib.so> [cfg3,cfg4]"""
+gpurun call and compare.  Usage: python tools/ab_pack.py <lib.so> [cfg3,cfg4,u64k,small]"""
 import ctypes as C
 import json
 import os
@@ -47,6 +47,9 @@ def main():
         elif cfg == "u64k":  # uniform 64 KiB frames, 8 GiB
             n = 1 << 17
             lens = np.full(n, 65536, np.int64)
+        elif cfg == "small":  # 8 M frames of 1-300 bytes (chat-sized messages)
+            n = 1 << 23
+            lens = rng.integers(1, 301, n).astype(np.int64)
         else:
             n = 4 << 20
             lens = np.full(n, 4096, np.int64)
