@@ -1037,14 +1037,25 @@ __global__ void __launch_bounds__(kBlock) chunk_map_kernel(const kmws_desc* __re
     }
 }
 
-struct ChunkFrame {  // one frame of a chunk's table (LDS), 32 B
-    uint64_t r0;     // region start in the output
-    uint64_t sdel;   // source byte - output byte over the payload (mod 2^64)
-    uint32_t len;
-    uint32_t key;    // key to apply (0 = none)
-    uint32_t hl;     // header bytes
-    uint32_t fl;     // flags (encode)
+// One frame of a chunk's table (LDS), 48 B: its geometry relative to the
+// chunk's first byte A0 (clamped to +-2^30: only offsets within a few bytes of
+// the chunk matter), its source pointer per output offset, the rotated key of
+// its aligned output words (byte x & 3 of it masks output byte x), and the
+// header bytes.
+struct ChunkFrame {
+    int32_t r0, p0, r1;  // region start, payload start, region end - A0
+    uint32_t rk;         // rot_key(key, p0) (0: no mask)
+    uint64_t sbase;      // source byte of output offset o = sbase + o
+    uint8_t h[16];       // the header's bytes (encode)
+    uint64_t pad;
 };
+static_assert(sizeof(ChunkFrame) == 48, "ChunkFrame is three 16-byte LDS loads");
+
+__device__ __forceinline__ int32_t rel32(uint64_t x, uint64_t A0)
+{
+    const int64_t d = (int64_t)(x - A0);
+    return d < -(1 << 30) ? -(1 << 30) : (d > (1 << 30) ? (1 << 30) : (int32_t)d);
+}
 
 // LDS written by some lanes of a wave and read by others: DS instructions of
 // one wave execute in order; this keeps the compiler from reordering them.
@@ -1071,33 +1082,18 @@ __device__ __forceinline__ void store_word_bytes(uint8_t* __restrict__ dst, uint
     }
 }
 
+template <bool NT>
 __device__ __forceinline__ u32x4 copy_src_load(const uint8_t* p)
 {
-#if KMWS_COPY_NT_LOAD
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-#else
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     return *reinterpret_cast<const u32x4*>(p);
-#endif
-}
-
-// Output byte x of frame e (x inside its region): a header byte
-// (WSHandler::encodeFrameHeader) or a masked payload byte.
-template <bool HEADERS>
-__device__ __forceinline__ uint32_t chunk_byte(const ChunkFrame& e, uint64_t x, const uint8_t* __restrict__ src)
-{
-    const uint64_t p0 = e.r0 + e.hl;
-    if (HEADERS && x < p0) {
-        uint64_t h0, h1;
-        build_header(e.len, e.fl, e.key, h0, h1);
-        const uint32_t k = (uint32_t)(x - e.r0);
-        return (uint32_t)((k < 8 ? h0 >> (8 * k) : h1 >> (8 * (k - 8))) & 0xFFu);
-    }
-    return src[x + e.sdel] ^ ((e.key >> (8 * ((x - p0) & 3u))) & 0xFFu);
 }
 
 // One wave per 4 KiB output chunk (4 words per lane, 1 KiB per instruction).
 // A chunk meeting more than kChunkFrames frames is listed for chunk_dense_kernel.
-template <bool HEADERS>
+// NT: non-temporal source loads (batches of large frames); ordinary loads keep
+// the source lines two neighbouring chunks share in the L2 (small frames).
+template <bool HEADERS, bool NT>
 __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                             const kmws_desc* __restrict__ d,
                                                             const uint16_t* __restrict__ flags, uint32_t n,
@@ -1108,8 +1104,8 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
                                                             uint32_t split)
 {
     __shared__ ChunkFrame s_tab[kBlock / 64][kChunkFrames];
-    __shared__ uint32_t s_slow[kBlock / 64][kChunkWords];
-    __shared__ u32x4 s_val[kBlock / 64][64 + 4];  // boundary words 0..63, then 4 scratch slots
+    __shared__ uint16_t s_slow[kBlock / 64][kChunkWords];  // boundary words: word | frame << 8
+    __shared__ u32x4 s_val[kBlock / 64][64 + 16];  // boundary words 0..63, then 16 scratch slots
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // consecutive blocks dealt over `split` parts of the output: with split 8,
@@ -1136,87 +1132,124 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
         const kmws_desc x = d[j];
         const uint32_t fl = HEADERS ? flags[j] : 0u;
         const uint32_t mask = HEADERS ? (fl >> 8) & 1u : 1u;
+        const uint64_t r0 = start[j], p0 = r0 + (HEADERS ? hdr_len(x.len, mask) : 0u);
+        const uint32_t key = mask ? x.key : 0u;
         ChunkFrame e;
-        e.r0 = start[j];
-        e.hl = HEADERS ? hdr_len(x.len, mask) : 0u;
-        e.sdel = x.off - (e.r0 + e.hl);
-        e.len = x.len;
-        e.key = mask ? x.key : 0u;
-        e.fl = fl;
+        e.r0 = rel32(r0, A0);
+        e.p0 = rel32(p0, A0);
+        e.r1 = rel32(p0 + x.len, A0);
+        e.rk = key ? rot_key(key, p0) : 0u;
+        e.sbase = (uint64_t)(uintptr_t)src + x.off - (p0 - A0);
+        uint64_t h0 = 0, h1 = 0;
+        if (HEADERS) build_header(x.len, fl, key, h0, h1);
+        __builtin_memcpy(e.h, &h0, 8);
+        __builtin_memcpy(e.h + 8, &h1, 8);
         tab[lane] = e;
     }
     wave_lds_sync();
+    const int32_t trel = total - A0 < kChunkBytes ? (int32_t)(total - A0) : (int32_t)kChunkBytes;  // live bytes
     // Pass 1: each word's frame (binary search over the table) and kind.  An
     // interior word lies inside one payload; it takes its second source word
     // from the next word's lane (lane 63: lane 0 of the next round) when that
-    // word is interior to the same payload.  Every other live word -- header
-    // bytes, a payload's first or last bytes, the last interior word before a
-    // boundary, the chunk's last word -- is listed as a boundary word.
-    uint32_t* sl = s_slow[wave];
-    uint32_t jbits = 0, slowbits = 0, nslow = 0;
+    // word is interior to the same payload, else from one extra load per lane
+    // (the chunk's last word, the last word of a payload; a lane whose words
+    // need two lists the second).  Every other live word -- header bytes, a
+    // payload's first or last bytes -- is listed as a boundary word.
+    uint16_t* sl = s_slow[wave];
+    uint32_t jbits = 0, slowbits = 0, nslow = 0, exr = kChunkW;  // exr: the round of the lane's extra load
 #pragma unroll
     for (int i = 0; i < (int)kChunkW; ++i) {
         const uint32_t k = 64u * i + lane;
-        const uint64_t a = A0 + 16ull * k;
+        const int32_t a = 16 * (int32_t)k;
         uint32_t lo = 0, hi = nfr;  // tab[lo].r0 <= a < tab[hi].r0
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (tab[mid].r0 <= a) lo = mid; else hi = mid;
         }
-        const ChunkFrame e = tab[lo];
-        const uint64_t p0 = e.r0 + e.hl, r1 = p0 + e.len;
-        const bool live = a < total;
+        const int32_t p0 = tab[lo].p0, r1 = tab[lo].r1;
+        const bool live = a < trel;
         const bool inner = live && a >= p0 && a + 16 <= r1;
-        const uint32_t delta = (uint32_t)((a + e.sdel) & 15u);
-        const bool fast = inner && (delta == 0 || (a + 32 <= r1 && (i + 1 < (int)kChunkW || lane != 63)));
+        const uint32_t delta = ((uint32_t)tab[lo].sbase + (uint32_t)a) & 15u;
+        const bool nb = delta == 0 || (a + 32 <= r1 && (i + 1 < (int)kChunkW || lane != 63));
+        const bool ex = inner && !nb && exr == kChunkW;
+        if (ex) exr = i;
+        const bool fast = inner && (nb || ex);
         const bool slow = live && !fast;
         const uint64_t bal = __ballot(slow);
-        if (slow) sl[nslow + lanes_below(bal)] = k | lo << 16;
+        if (slow) sl[nslow + lanes_below(bal)] = (uint16_t)(k | lo << 8);
         jbits |= lo << (6 * i);
         slowbits |= slow ? 1u << i : 0u;
         nslow += (uint32_t)__builtin_popcountll(bal);
     }
     wave_lds_sync();
-    // Pass 2: interior words' source words, one aligned word each (all four
-    // rounds issued before anything waits).
-    u32x4 L0[kChunkW];
-    uint32_t rk[kChunkW], dl = 0;
-#pragma unroll
-    for (int i = 0; i < (int)kChunkW; ++i) {
-        const uint64_t a = A0 + 16ull * (64u * i + lane);
-        const ChunkFrame e = tab[(jbits >> (6 * i)) & 63u];
-        const uint64_t p0 = e.r0 + e.hl, r1 = p0 + e.len;
-        const bool inner = a < total && a >= p0 && a + 16 <= r1;
-        const uint64_t sa = a + e.sdel;
-        L0[i] = copy_src_load(src + (inner ? sa & ~15ull : 0));
-        dl |= (uint32_t)(sa & 15u) << (4 * i);
-        rk[i] = e.key ? rot_key(e.key, p0) : 0u;
-    }
-    // Pass 3: boundary words, byte-parallel -- four words at a time, one lane
-    // per byte (its frame found from the word's first frame on; a header byte
-    // or a masked source byte), assembled in LDS.  The first 64 join the stores
-    // of pass 4; more (chunks of many small frames) are stored here.
+    // Boundary words are composed byte-parallel: one lane per byte, 16 words
+    // per batch (four per instruction).  Each byte's frame is found from its
+    // word's first frame on; the byte is a header byte (from the table) or a
+    // masked source byte.  The first batch's source bytes are loaded before the
+    // interior words' (pass 2), so one latency covers both.  Words are
+    // assembled in LDS: the first 64 join the stores of pass 4, later ones
+    // (chunks of many small frames) are stored by their batch.
     uint8_t* sb = reinterpret_cast<uint8_t*>(&s_val[wave][0]);
-    for (uint32_t g0 = 0; g0 < nslow; g0 += 4) {  // wave-uniform
-        const uint32_t qi = g0 + ((uint32_t)lane >> 4), bi = lane & 15;
-        if (qi < nslow) {
-            const uint32_t ent = sl[qi];
-            uint32_t m = ent >> 16;
-            const uint64_t x = A0 + 16ull * (ent & 0xFFFFu) + bi;
+    uint32_t hv[4], sv[4];
+    auto batch_issue = [&](uint32_t g0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t qi = g0 + 4u * u + ((uint32_t)lane >> 4);
+            const uint32_t ent = qi < nslow ? sl[qi] : 0u;
+            uint32_t m = ent >> 8;
+            const int32_t x = 16 * (int32_t)(ent & 0xFFu) + (lane & 15);
             while (m + 1 < nfr && tab[m + 1].r0 <= x) ++m;
-            const uint32_t v = x < total ? chunk_byte<HEADERS>(tab[m], x, src) : 0u;
-            sb[16u * (qi < 64 ? qi : 64 + ((uint32_t)lane >> 4)) + bi] = (uint8_t)v;
+            const ChunkFrame& e = tab[m];
+            const bool live = qi < nslow && x < trel;
+            const bool hdr = HEADERS && x < e.p0;
+            if (hdr)  // header byte x - r0 (< 14); bit 8: no source byte
+                hv[u] = 0x100u | e.h[live ? (uint32_t)(x - e.r0) & 15u : 0u];
+            else  // the key byte of output byte x
+                hv[u] = (e.rk >> (8 * (x & 3))) & 0xFFu;
+            sv[u] = *reinterpret_cast<const uint8_t*>(live && !hdr ? e.sbase + (int64_t)x : (uint64_t)(uintptr_t)src);
         }
-        if (g0 >= 64) {  // wave-uniform: four words past the first 64, stored now
+    };
+    auto batch_put = [&](uint32_t g0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t qi = g0 + 4u * u + ((uint32_t)lane >> 4);
+            const uint32_t v = (hv[u] & 0x100u) ? hv[u] : (sv[u] ^ hv[u]);
+            if (qi < nslow) sb[16u * (qi < 64 ? qi : 64 + 4u * u + ((uint32_t)lane >> 4)) + (lane & 15)] = (uint8_t)v;
+        }
+        if (g0 >= 64) {  // wave-uniform: sixteen words past the first 64, stored now
             wave_lds_sync();
-            if (lane < 4 && g0 + lane < nslow) {
-                const uint64_t a = A0 + 16ull * (sl[g0 + lane] & 0xFFFFu);
+            if (lane < 16 && g0 + lane < nslow) {
+                const uint64_t a = A0 + 16ull * (sl[g0 + lane] & 0xFFu);
                 const u32x4 v = s_val[wave][64 + lane];
                 if (a + 16 <= total) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + a));
                 else store_word_bytes(dst, a, total, v);
             }
             wave_lds_sync();  // the scratch slots are reused
         }
+    };
+    if (nslow) batch_issue(0);
+    // Pass 2: interior words' source words, one aligned word each (all four
+    // rounds issued before anything waits).
+    u32x4 L0[kChunkW], X;
+    uint32_t rk[kChunkW], dl = 0;
+    uint64_t xa = (uint64_t)(uintptr_t)src;
+#pragma unroll
+    for (int i = 0; i < (int)kChunkW; ++i) {
+        const int32_t a = 16 * (int32_t)(64u * i + lane);
+        const ChunkFrame& e = tab[(jbits >> (6 * i)) & 63u];
+        const bool inner = a < trel && a >= e.p0 && a + 16 <= e.r1;
+        const uint64_t sa = e.sbase + (int64_t)a;
+        L0[i] = copy_src_load<NT>(inner ? reinterpret_cast<const uint8_t*>(sa & ~15ull) : src);
+        if (exr == (uint32_t)i) xa = (sa + 15) & ~15ull;  // the aligned word holding the word's last source byte
+        dl |= (uint32_t)(sa & 15u) << (4 * i);
+        rk[i] = e.rk;
+    }
+    X = copy_src_load<NT>(reinterpret_cast<const uint8_t*>(xa));
+    // Pass 3: the boundary words
+    if (nslow) batch_put(0);
+    for (uint32_t g0 = 16; g0 < nslow; g0 += 16) {  // wave-uniform
+        batch_issue(g0);
+        batch_put(g0);
     }
     wave_lds_sync();
     // Pass 4: the four full-width stores, boundary words merged in.
@@ -1230,6 +1263,7 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
             const u32x4 nx = readlane0(L0[i + 1 < (int)kChunkW ? i + 1 : i]);
             if (lane == 63) hi = nx;
         }
+        if (exr == (uint32_t)i) hi = X;
         u32x4 out = funnel16(L0[i], hi, (dl >> (4 * i)) & 15u) ^ rk[i];
         const bool slow = (slowbits >> i) & 1u;
         const uint64_t bal = __ballot(slow);
@@ -1736,6 +1770,22 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 #ifndef KMWS_PACK_UNITS
 #define KMWS_PACK_UNITS 0
 #endif
+// Chunk copy tuning by the mean region bound cap / n (tuning builds override):
+// non-temporal source loads from KMWS_CHUNK_NT_FROM bytes (measured: faster
+// for every batch, cfg4 0.77 / 0.79 against 0.76 / 0.76 encode / gather with
+// ordinary loads; profiles/r04o_chunk_ab.txt), and from KMWS_CHUNK_PAD_FROM
+// bytes KMWS_CHUNK_PAD_BYTES of dynamic LDS per block (19 KiB static + 13 KiB:
+// 5 blocks per CU -- the unit form's large-frame setting, 0.61 against 0.75 on
+// cfg3 here, so never by default).
+#ifndef KMWS_CHUNK_NT_FROM
+#define KMWS_CHUNK_NT_FROM 0
+#endif
+#ifndef KMWS_CHUNK_PAD_FROM
+#define KMWS_CHUNK_PAD_FROM 0xFFFFFFFFFFFFFFFFull
+#endif
+#ifndef KMWS_CHUNK_PAD_BYTES
+#define KMWS_CHUNK_PAD_BYTES 13312
+#endif
 struct CopyWs {
     WsHead* head;
     V2* tiles;  // ntiles + 1: tile prefixes, then the totals
@@ -1846,11 +1896,22 @@ static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t c
         const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
         constexpr uint64_t kWaves = kBlock / 64;
         constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
+        // cap / n bounds the mean region size from above: runs of large frames
+        // stream faster with non-temporal loads and fewer blocks per CU (fewer
+        // concurrent DRAM streams), batches of small frames with ordinary loads
+        // and every wave slot
+        const uint64_t mean = cap / n;
+        const bool nt_loads = mean >= (uint64_t)KMWS_CHUNK_NT_FROM;
+        const unsigned lds_pad = mean >= (uint64_t)KMWS_CHUNK_PAD_FROM ? (unsigned)KMWS_CHUNK_PAD_BYTES : 0u;
         for (uint64_t c0 = 0; c0 < chunks; c0 += kMaxChunksPerLaunch) {
             const uint64_t nc = chunks - c0 < kMaxChunksPerLaunch ? chunks - c0 : kMaxChunksPerLaunch;
-            hipLaunchKernelGGL(chunk_copy_kernel<HEADERS>, dim3((uint32_t)((nc + kWaves - 1) / kWaves)), dim3(kBlock),
-                               0, s, src, dst, d, flags, n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0,
-                               kCopySplit);
+            const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
+            if (nt_loads)
+                hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
+                                   n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
+            else
+                hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d,
+                                   flags, n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
         }
         const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
         hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n,

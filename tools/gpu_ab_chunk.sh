@@ -1,11 +1,11 @@
 #!/bin/bash
 # The copy path's chunk form (product: chunk_map + chunk_copy) checked and
-# timed against the round-3 unit form, RUN_TAG=<tag>:
+# timed, RUN_TAG=<tag>:
 #  1. the pack / configs / fuzz GPU tests on the product build;
 #  2. tools/ab_pack.py (cfg4, cfg3, small frames) per build, each loaded alone:
-#     product (chunk, non-temporal source loads), tools/ab/libkmws_chunk_tl.so
-#     (chunk, ordinary loads), tools/ab/libkmws_units.so (KMWS_PACK_UNITS=1),
-#     tools/ab/libkmws_tload.so (units, ordinary loads).
+#     product (non-temporal source loads), tools/ab/libkmws_alltl.so
+#     (ordinary loads), _units.so (round 3's unit form, KMWS_PACK_UNITS=1);
+#  3. FETCH_SIZE and WRITE_SIZE passes (separate runs) of the product on cfg4.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${RUN_TAG:?set RUN_TAG}
@@ -14,7 +14,13 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread \
     tests/test_gpu_pack.py tests/test_gpu_configs.py tests/test_gpu_fuzz.py > "$OUT/pytest_pack.log" 2>&1 &&
-for v in product:kuma_amd/lib/libkmws_gpu.so chunk_tl:tools/ab/libkmws_chunk_tl.so units:tools/ab/libkmws_units.so \
-         tload:tools/ab/libkmws_tload.so; do
+for v in product:kuma_amd/lib/libkmws_gpu.so alltl:tools/ab/libkmws_alltl.so units:tools/ab/libkmws_units.so; do
   timeout -k 10 240 python3 tools/ab_pack.py "${v#*:}" cfg4,cfg3,small > "$OUT/ab_${v%%:*}.json" 2> "$OUT/ab_${v%%:*}.err" || exit 1
-done
+done &&
+pass() {  # dir counter
+  timeout -k 10 -s KILL 150 rocprofv3 --pmc "$2" --kernel-trace --output-format csv -d "$PWD/$OUT/$1" -o run -- \
+    python3 tools/ab_pack.py kuma_amd/lib/libkmws_gpu.so cfg4 > "$OUT/$1.json" 2> "$OUT/$1.err"
+} &&
+pass pmc_fetch FETCH_SIZE &&
+pass pmc_write WRITE_SIZE &&
+python3 tools/pmc_kernels.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_cfg4_pack_kernels.txt"
