@@ -983,9 +983,15 @@ __device__ __forceinline__ u32x4 shfl16_down1(const u32x4& v)
 // more fetched on cfg4) and wrote 80 B of edge words and two
 // 32 B unit records per 4 KiB frame; here their values join the chunk's four
 // full-width stores through LDS.
-constexpr uint64_t kChunkBytes = 4096;
-constexpr uint32_t kChunkWords = (uint32_t)(kChunkBytes / 16);
-constexpr uint32_t kChunkW = kChunkWords / 64;  // words per lane
+#ifndef KMWS_CHUNK_LANE_WORDS
+#define KMWS_CHUNK_LANE_WORDS 4
+#endif
+constexpr uint32_t kChunkW = KMWS_CHUNK_LANE_WORDS;  // words per lane (4 or 8)
+constexpr uint32_t kChunkWords = 64 * kChunkW;
+constexpr uint64_t kChunkBytes = 16ull * kChunkWords;
+constexpr uint32_t kSlowShift = 9;  // boundary-list entry: word | table frame << kSlowShift
+constexpr uint32_t kSlowWord = (1u << kSlowShift) - 1;
+static_assert(kChunkW == 4 || kChunkW == 8, "chunk: 4 or 8 words per lane");
 constexpr uint32_t kChunkFrames = 64;           // a chunk's frame table, one lane per frame
 
 __host__ __device__ __forceinline__ uint64_t chunk_count(uint64_t bytes) { return (bytes + kChunkBytes - 1) / kChunkBytes; }
@@ -1104,7 +1110,7 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
                                                             uint32_t split)
 {
     __shared__ ChunkFrame s_tab[kBlock / 64][kChunkFrames];
-    __shared__ uint16_t s_slow[kBlock / 64][kChunkWords];  // boundary words: word | frame << 8
+    __shared__ uint16_t s_slow[kBlock / 64][kChunkWords];  // boundary words: word | frame << kSlowShift
     __shared__ u32x4 s_val[kBlock / 64][64 + 16];  // boundary words 0..63, then 16 scratch slots
     const int lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1156,7 +1162,8 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
     // need two lists the second).  Every other live word -- header bytes, a
     // payload's first or last bytes -- is listed as a boundary word.
     uint16_t* sl = s_slow[wave];
-    uint32_t jbits = 0, slowbits = 0, nslow = 0, exr = kChunkW;  // exr: the round of the lane's extra load
+    uint64_t jbits = 0;
+    uint32_t slowbits = 0, nslow = 0, exr = kChunkW;  // exr: the round of the lane's extra load
 #pragma unroll
     for (int i = 0; i < (int)kChunkW; ++i) {
         const uint32_t k = 64u * i + lane;
@@ -1176,8 +1183,8 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
         const bool fast = inner && (nb || ex);
         const bool slow = live && !fast;
         const uint64_t bal = __ballot(slow);
-        if (slow) sl[nslow + lanes_below(bal)] = (uint16_t)(k | lo << 8);
-        jbits |= lo << (6 * i);
+        if (slow) sl[nslow + lanes_below(bal)] = (uint16_t)(k | lo << kSlowShift);
+        jbits |= (uint64_t)lo << (6 * i);
         slowbits |= slow ? 1u << i : 0u;
         nslow += (uint32_t)__builtin_popcountll(bal);
     }
@@ -1196,8 +1203,8 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
         for (int u = 0; u < 4; ++u) {
             const uint32_t qi = g0 + 4u * u + ((uint32_t)lane >> 4);
             const uint32_t ent = qi < nslow ? sl[qi] : 0u;
-            uint32_t m = ent >> 8;
-            const int32_t x = 16 * (int32_t)(ent & 0xFFu) + (lane & 15);
+            uint32_t m = ent >> kSlowShift;
+            const int32_t x = 16 * (int32_t)(ent & kSlowWord) + (lane & 15);
             while (m + 1 < nfr && tab[m + 1].r0 <= x) ++m;
             const ChunkFrame& e = tab[m];
             const bool live = qi < nslow && x < trel;
@@ -1219,7 +1226,7 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
         if (g0 >= 64) {  // wave-uniform: sixteen words past the first 64, stored now
             wave_lds_sync();
             if (lane < 16 && g0 + lane < nslow) {
-                const uint64_t a = A0 + 16ull * (sl[g0 + lane] & 0xFFu);
+                const uint64_t a = A0 + 16ull * (sl[g0 + lane] & kSlowWord);
                 const u32x4 v = s_val[wave][64 + lane];
                 if (a + 16 <= total) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + a));
                 else store_word_bytes(dst, a, total, v);
@@ -1236,7 +1243,7 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
 #pragma unroll
     for (int i = 0; i < (int)kChunkW; ++i) {
         const int32_t a = 16 * (int32_t)(64u * i + lane);
-        const ChunkFrame& e = tab[(jbits >> (6 * i)) & 63u];
+        const ChunkFrame& e = tab[(uint32_t)(jbits >> (6 * i)) & 63u];
         const bool inner = a < trel && a >= e.p0 && a + 16 <= e.r1;
         const uint64_t sa = e.sbase + (int64_t)a;
         L0[i] = copy_src_load<NT>(inner ? reinterpret_cast<const uint8_t*>(sa & ~15ull) : src);
@@ -1764,12 +1771,26 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 }
 
 // ------------------------------ host launchers ------------------------------
-// The copy form: chunk_map + chunk_copy (product), or the round-3 form --
-// prologue (edge words, unit records) + copy_kernel -- in a tuning build
-// (KMWS_PACK_UNITS=1) for A/B runs.
+// The copy form, by the mean region bound cap / n: below KMWS_PACK_CHUNK_BELOW
+// bytes the chunk form (chunk_map + chunk_copy), from it the unit form
+// (prologue: edge words, unit records; copy_kernel).  Measured on one box
+// (profiles/r04p_chunk_ab.txt): cfg4 (4 KiB frames) 0.748 / 0.772 chunk against
+// 0.722 / 0.741 units, 8 M frames of 1-300 B 0.38 / 0.48 against 0.055 /
+// 0.058, cfg3 (Zipf, 37 KiB mean, 97 % of the bytes in frames >= 16 KiB)
+// 0.733 / 0.776 against 0.775 / 0.797 (encode / gather).  Tuning builds:
+// KMWS_PACK_UNITS=1 forces the unit form, KMWS_PACK_UNITS=2 the chunk form.
 #ifndef KMWS_PACK_UNITS
 #define KMWS_PACK_UNITS 0
 #endif
+#ifndef KMWS_PACK_CHUNK_BELOW
+#define KMWS_PACK_CHUNK_BELOW 16384
+#endif
+static bool use_chunks(uint32_t n, uint64_t cap)
+{
+    if (KMWS_PACK_UNITS == 1) return false;
+    if (KMWS_PACK_UNITS == 2) return true;
+    return n && cap / n < (uint64_t)KMWS_PACK_CHUNK_BELOW;
+}
 // Chunk copy tuning by the mean region bound cap / n (tuning builds override):
 // non-temporal source loads from KMWS_CHUNK_NT_FROM bytes (measured: faster
 // for every batch, cfg4 0.77 / 0.79 against 0.76 / 0.76 encode / gather with
@@ -1823,12 +1844,10 @@ static void carve_scan(char* p, uint32_t n, CopyWs& c)
 
 static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
-#if KMWS_PACK_UNITS
-    return r256(scan_ws_size(n)) + r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
-#else
+    if (!use_chunks(n, cap))
+        return r256(scan_ws_size(n)) + r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
     return r256(scan_ws_size(n)) + r256((chunk_count(cap) + 1) * sizeof(uint32_t)) +
            r256(chunk_count(cap) * sizeof(uint32_t));
-#endif
 }
 
 static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c)
@@ -1881,6 +1900,36 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
 // mean from above) runs batches of small frames through the fused row kernel
 // instead: measured slower on cfg4 (0.64 vs 0.72 of HBM peak,
 // profiles/r04i_pack_rows_ab.txt), so the product never does.
+// The chunk form after the scan: chunk_map, the chunk copy grid, the dense
+// chunks (usually none: the grid of chunk_dense_kernel exits at once).
+template <bool HEADERS>
+static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
+                                 const uint16_t* flags, uint32_t n, CopyWs& c, uint32_t nt, hipStream_t s)
+{
+    hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, d, flags, n, cap,
+                       c.head, c.tiles, nt, c.grp, start, c.cmap);
+    const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
+    constexpr uint64_t kWaves = kBlock / 64;
+    constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
+    const uint64_t mean = cap / n;  // bounds the mean region size from above
+    const bool nt_loads = mean >= (uint64_t)KMWS_CHUNK_NT_FROM;
+    const unsigned lds_pad = mean >= (uint64_t)KMWS_CHUNK_PAD_FROM ? (unsigned)KMWS_CHUNK_PAD_BYTES : 0u;
+    for (uint64_t c0 = 0; c0 < chunks; c0 += kMaxChunksPerLaunch) {
+        const uint64_t nc = chunks - c0 < kMaxChunksPerLaunch ? chunks - c0 : kMaxChunksPerLaunch;
+        const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
+        if (nt_loads)
+            hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags, n,
+                               start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
+        else
+            hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
+                               n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
+    }
+    const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
+    hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n, start,
+                       c.cmap, c.tiles + nt, c.head, c.dense);
+    return hip_status(hipGetLastError());
+}
+
 #ifndef KMWS_PACK_ROWS_MAX_MEAN
 #define KMWS_PACK_ROWS_MAX_MEAN 0
 #endif
@@ -1889,36 +1938,7 @@ static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t c
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t nt = (uint32_t)n_tiles(n);
-#if !KMWS_PACK_UNITS
-    hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, d, flags, n, cap,
-                       c.head, c.tiles, nt, c.grp, start, c.cmap);
-    {
-        const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
-        constexpr uint64_t kWaves = kBlock / 64;
-        constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
-        // cap / n bounds the mean region size from above: runs of large frames
-        // stream faster with non-temporal loads and fewer blocks per CU (fewer
-        // concurrent DRAM streams), batches of small frames with ordinary loads
-        // and every wave slot
-        const uint64_t mean = cap / n;
-        const bool nt_loads = mean >= (uint64_t)KMWS_CHUNK_NT_FROM;
-        const unsigned lds_pad = mean >= (uint64_t)KMWS_CHUNK_PAD_FROM ? (unsigned)KMWS_CHUNK_PAD_BYTES : 0u;
-        for (uint64_t c0 = 0; c0 < chunks; c0 += kMaxChunksPerLaunch) {
-            const uint64_t nc = chunks - c0 < kMaxChunksPerLaunch ? chunks - c0 : kMaxChunksPerLaunch;
-            const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
-            if (nt_loads)
-                hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
-                                   n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
-            else
-                hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d,
-                                   flags, n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
-        }
-        const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
-        hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n,
-                           start, c.cmap, c.tiles + nt, c.head, c.dense);
-    }
-    return hip_status(hipGetLastError());
-#else
+    if (use_chunks(n, cap)) return launch_chunks<HEADERS>(src, dst, cap, start, d, flags, n, c, nt, s);
 #if KMWS_PACK_ROWS_MAX_MEAN > 0
     if (cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
         hipLaunchKernelGGL(pack_rows_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, dst, d, flags,
@@ -1942,7 +1962,6 @@ static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t c
                            dim3(kBlock), lds_pad, s, src, dst, c.tiles + nt, c.rec, c.edge, c.head, u0, kCopySplit);
     }
     return hip_status(hipGetLastError());
-#endif
 }
 
 }  // namespace kmws

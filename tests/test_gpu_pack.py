@@ -131,7 +131,11 @@ def wire_and_offsets(rng, kind, n, mode_mask=1):
 
 
 @pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max"])
-def test_unpack_gather_roundtrip(T, kind):
+@pytest.mark.parametrize("room", [0, 20000])
+def test_unpack_gather_roundtrip(T, kind, room):
+    """room = spare arena capacity per frame: 20000 puts the mean region bound
+    past 16 KiB, so the gather takes the unit form; 0 the chunk form for every
+    kind with a smaller mean (kmws_pack.hip, use_chunks)."""
     from kuma_amd import kmws
     rng = np.random.default_rng(zlib.crc32(str(kind).encode()))
     wire, wire_off, src, offs, lens, flags, keys = wire_and_offsets(rng, kind, 250 if kind != "max" else 6)
@@ -167,13 +171,14 @@ def test_unpack_gather_roundtrip(T, kind):
                                     (f.mask << 8) for f in ofr]
     # gather + unmask into a dense arena == the oracle's payloads == the original source bytes
     total = int(dd["len"].sum())
-    dst = T.zeros(total + 32, dtype=T.uint8, device="cuda")
+    dst = T.zeros(total + 32 + room * n, dtype=T.uint8, device="cuda")
     dst_off = T.zeros(n + 1, dtype=T.int64, device="cuda")
     ws2 = kmws.Workspace(kmws.copy_workspace_size(n, dst.numel()))
     kmws.gather_unmask(d_wire, out_desc, dst, dst_off, ws2)
     T.cuda.synchronize()
     assert ws2.status() == 0
     assert bytes(dst.cpu().numpy()[:total]) == b"".join(f.payload for f in ofr)
+    assert int(dst[total:].count_nonzero()) == 0  # nothing written past the arena's payloads
     orig = b"".join(bytes(src[int(o):int(o) + int(L)]) for o, L in zip(offs[:n], lens[:n]))
     assert bytes(dst.cpu().numpy()[:total]) == orig
     # in-place alternative: unmask the wire itself with the unpacked descriptors

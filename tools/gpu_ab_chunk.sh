@@ -3,8 +3,9 @@
 # timed, RUN_TAG=<tag>:
 #  1. the pack / configs / fuzz GPU tests on the product build;
 #  2. tools/ab_pack.py (cfg4, cfg3, small frames) per build, each loaded alone:
-#     product (non-temporal source loads), tools/ab/libkmws_alltl.so
-#     (ordinary loads), _units.so (round 3's unit form, KMWS_PACK_UNITS=1);
+#     product (chunk form below a 16 KiB mean region, unit form above),
+#     tools/ab/libkmws_chunks.so (chunk form always, KMWS_PACK_UNITS=2),
+#     _units.so (unit form always, KMWS_PACK_UNITS=1);
 #  3. FETCH_SIZE and WRITE_SIZE passes (separate runs) of the product on cfg4.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,7 +15,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread \
     tests/test_gpu_pack.py tests/test_gpu_configs.py tests/test_gpu_fuzz.py > "$OUT/pytest_pack.log" 2>&1 &&
-for v in product:kuma_amd/lib/libkmws_gpu.so alltl:tools/ab/libkmws_alltl.so units:tools/ab/libkmws_units.so; do
+for v in product:kuma_amd/lib/libkmws_gpu.so chunks:tools/ab/libkmws_chunks.so units:tools/ab/libkmws_units.so; do
   timeout -k 10 240 python3 tools/ab_pack.py "${v#*:}" cfg4,cfg3,small > "$OUT/ab_${v%%:*}.json" 2> "$OUT/ab_${v%%:*}.err" || exit 1
 done &&
 pass() {  # dir counter
