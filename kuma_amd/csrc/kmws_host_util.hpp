@@ -161,10 +161,8 @@ public:
         (void)hipGetLastError();
         return true;  // finished, or failed: wait() reports which
     }
-    // Spins on the event for up to kSpinWaitUs first: hipEventSynchronize
-    // parks the thread, and waking it costs more than a small job (measured on
-    // the loopback cfg1 flush: 1.0 GiB/s parked vs 2.2 polled).  Longer jobs
-    // then park.
+    // Spins on the event for up to kSpinWaitUs first (a loop thread waiting for
+    // a small job should not be parked and woken by the runtime), then parks.
     kmws_status wait()
     {
         if (!launched_) return KMWS_OK;

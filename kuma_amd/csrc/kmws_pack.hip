@@ -91,6 +91,10 @@ constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
 #define KMWS_COPY_SPLIT_DEFAULT 8  // re-measured on plain allocations this round: 2 / 4 / 16 / XCD runs all slower
 #endif                              // on cfg4 and cfg3 (profiles/r03bi_copy_split_ab.txt)
 constexpr uint32_t kCopySplit = KMWS_COPY_SPLIT_DEFAULT;
+#ifndef KMWS_CHUNK_SPLIT
+#define KMWS_CHUNK_SPLIT 4  // the chunk grid's parts (r04r: 4 > 8 > 16 on cfg4)
+#endif
+constexpr uint32_t kChunkSplit = KMWS_CHUNK_SPLIT;
 constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
 #ifndef KMWS_LINE_BYTES
 #define KMWS_LINE_BYTES 64
@@ -1919,10 +1923,10 @@ static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap,
         const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
         if (nt_loads)
             hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags, n,
-                               start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
+                               start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
         else
             hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
-                               n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kCopySplit);
+                               n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
     }
     const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
     hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n, start,
