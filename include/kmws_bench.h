@@ -57,13 +57,14 @@ kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t se
                                 const kmws_desc* descs, uint32_t n,
                                 unsigned long long* mismatches, void* stream);
 
-/* The resident worker of the calling thread on `device` (kmws_resident.hip),
- * which serves the synchronous host entries (kmws_decoder_feed,
- * kmws_mask_host_chain) without a launch per call.  enable(0) makes this
- * thread's calls launch a kernel per call instead (the A/B of bench.py cfg1);
- * info: jobs served, launches (incarnations) so far, and whether it is on the
- * GPU now (it exits after 5 ms without a job; until then a device-wide
- * synchronize such as torch.cuda.synchronize waits for it). */
+/* The resident worker on `device` (kmws_resident.hip): one per device, shared
+ * by the process's threads, which serves the synchronous host entries
+ * (kmws_decoder_feed, kmws_mask_host_chain; jobs of <= 128 payloads and
+ * <= 64 KiB) without a launch per call.  enable(0) makes the CALLING thread's
+ * calls launch a kernel per call instead (the A/B of bench.py cfg1); info: jobs
+ * served, launches (incarnations) so far, and whether it is on the GPU now (it
+ * exits 200 us after its last job and after a 1 ms lease; until then a
+ * device-wide synchronize such as torch.cuda.synchronize waits for it). */
 kmws_status kmws_resident_enable(int device, int on);
 kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, int* running);
 

@@ -101,7 +101,12 @@ kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const Pi
 // kResMaxDescs payloads and kResMaxBytes bytes go to a workgroup that stays on
 // the GPU polling pinned memory, instead of a launch + wait per call.
 constexpr int kResMaxDescs = 128;
-constexpr uint64_t kResMaxBytes = 1u << 20;
+// One workgroup moves a job over PCIe at ~3 GB/s: at 64 KiB it is as fast as a
+// launch of the multi-block pieces kernel (20 us each, tests/cpp/rx_flush_bench.cpp,
+// profiles/r04w_rx_flush_bench.jsonl), below it faster (10.7 vs 18.5 us at 16
+// KiB), above it slower (the loopback cfg1 receive loop flushing 64-256 KiB
+// ran at 0.9-1.0 GiB/s on the worker against 2.0 launched, r04x).
+constexpr uint64_t kResMaxBytes = 64u << 10;
 // Unmasks descs[0..n) over dev_base and descs2[0..n2) over dev_base2 (device
 // views of pinned host memory, offsets relative to them), synchronously.
 // KMWS_ERR_NOT_SUPPORTED: too large for one job, or no worker on this thread

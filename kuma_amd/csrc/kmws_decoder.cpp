@@ -618,7 +618,7 @@ kmws_status kmws_tx_batch_attach_ring(kmws_tx_batch* b, uint8_t* ring, size_t ri
 // the attached pinned ring are masked in place there, the others gathered
 // into pinned staging and copied back when the generation completes; one
 // launch per buffer -- or, for a flush (sync), one synchronous job on the
-// thread's resident worker (kmws_resident.hip) when it fits one.
+// device's resident worker (kmws_resident.hip) when it fits one.
 static int64_t tx_submit(kmws_tx_batch* b, bool sync)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
@@ -796,7 +796,7 @@ void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
             if (it.dec == dec) it.live = false;
 }
 
-// sync (a flush): one synchronous job on the thread's resident worker when it
+// sync (a flush): one synchronous job on the device's resident worker when it
 // fits one (else a launch and a wait), instead of an enqueued launch.
 static int rx_submit(kmws_rx_batch* b, bool sync)
 {

@@ -127,7 +127,7 @@ public:
     // buffer of extra_span bytes, if given), then wait for the GPU.  One launch
     // per buffer (launch_unmask_pieces) reading descriptors and piece list from
     // pinned memory: no plan kernels, no copies, no status read-back.
-    // Small jobs go to this thread's resident worker (no launch, no event wait;
+    // Small jobs go to the device's resident worker (no launch, no event wait;
     // kmws_resident.hip); larger ones are launched on the stage's stream.
     // extra_dv: the device view of extra_base if the caller has it (a ring
     // attached once); else it is looked up here (hipPointerGetAttributes).

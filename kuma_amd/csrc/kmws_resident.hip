@@ -8,7 +8,10 @@
 // event wait costs 13-15 us per call -- about what kuma's byte loop
 // (WSHandler.cpp:303-310) spends on a whole 64 KiB read -- so the synchronous
 // drop-in lost to the reference.  Here one workgroup of 1024
-// lanes stays resident on the GPU per host thread and device and polls a
+// lanes stays resident on the GPU per device -- shared by the process's host
+// threads, one job at a time under a spin lock (a worker per thread measured
+// worse: two workers' streams share a hardware queue, so one thread's job
+// waited for the other's worker to leave, up to its lease) -- and polls a
 // mailbox in pinned host memory: the host writes a job (up to kResMaxDescs
 // payloads, each a device-visible address, a length and a key) and bumps the
 // job number; the worker sees it over PCIe, unmasks every payload in place
@@ -251,16 +254,27 @@ namespace {
 
 void quit_all_workers();
 
-// One per (host thread, device).  Never freed: releasing pinned memory from a
-// thread_local destructor can run after the HIP runtime was torn down.  At
-// process exit an atexit handler -- registered after the HIP runtime's own,
-// so it runs before the runtime's teardown -- asks every worker to quit and
-// waits (bounded) until each running kernel has exited: the grid has drained
-// before the process ends.  The idle exit ends a worker whose thread stopped
-// feeding.
+// One per device, shared by every host thread: a job holds the worker's spin
+// lock from posting its descriptors to seeing it done (jobs take microseconds;
+// the kernel serves one at a time anyway).  Never freed: releasing pinned
+// memory from a static destructor can run after the HIP runtime was torn
+// down.  At process exit an atexit handler -- registered after the HIP
+// runtime's own, so it runs before the runtime's teardown -- asks every
+// worker to quit and waits (bounded) until each running kernel has exited:
+// the grid has drained before the process ends.  The idle exit ends a worker
+// nobody feeds.
 class ResidentWorker {
 public:
     explicit ResidentWorker(int device) : device_(device) {}
+
+    void lock()
+    {
+        for (;;) {
+            if (!__atomic_exchange_n(&busy_, true, __ATOMIC_ACQUIRE)) return;
+            while (__atomic_load_n(&busy_, __ATOMIC_RELAXED)) cpu_relax();
+        }
+    }
+    void unlock() { __atomic_store_n(&busy_, false, __ATOMIC_RELEASE); }
 
     // Ask the kernel to leave at its next poll and wait for it (atexit).
     void quit_and_wait()
@@ -273,14 +287,15 @@ public:
             cpu_relax();
     }
 
+    // (under the lock) created on first use: a process whose threads all
+    // switched the worker off creates nothing (no stream, no mailbox)
     bool usable()
     {
         if (state_ == 0) state_ = init() == KMWS_OK ? 1 : -1;
-        return state_ == 1 && enabled_;
+        return state_ == 1;
     }
-    void set_enabled(bool on) { enabled_ = on; }
 
-    // One synchronous job of n <= kResMaxDescs payloads.
+    // One synchronous job of n <= kResMaxDescs payloads (under the lock).
     kmws_status run(const ResDesc* d, uint32_t n)
     {
         if (n == 0) return KMWS_OK;
@@ -387,8 +402,8 @@ private:
     }
 
     int device_;
-    int state_ = 0;  // 0 untried, 1 ready, -1 unusable
-    bool enabled_ = true;
+    bool busy_ = false;  // the spin lock
+    int state_ = 0;      // 0 untried, 1 ready, -1 unusable
     bool running_ = false;
     ResMailbox* mb_ = nullptr;
     ResMailbox* dmb_ = nullptr;
@@ -408,21 +423,30 @@ void quit_all_workers()
         for (ResidentWorker* w : *g_all) w->quit_and_wait();
 }
 
+constexpr int kMaxDevices = 64;
+ResidentWorker* g_by_dev[kMaxDevices];  // set once under g_all_mu, read with acquire loads
+
 ResidentWorker* worker(int device)
 {
-    static thread_local std::vector<ResidentWorker*> by_dev;
-    if (device < 0 || device > 1024) return nullptr;
-    if ((size_t)device >= by_dev.size()) by_dev.resize(device + 1, nullptr);
-    if (!by_dev[device]) {
-        ResidentWorker* w = new (std::nothrow) ResidentWorker(device);
+    if (device < 0 || device >= kMaxDevices) return nullptr;
+    ResidentWorker* w = __atomic_load_n(&g_by_dev[device], __ATOMIC_ACQUIRE);
+    if (w) return w;
+    std::lock_guard<std::mutex> lk(g_all_mu);
+    w = g_by_dev[device];
+    if (!w) {
+        w = new (std::nothrow) ResidentWorker(device);
         if (!w) return nullptr;
-        std::lock_guard<std::mutex> lk(g_all_mu);
         if (!g_all) g_all = new std::vector<ResidentWorker*>();
         g_all->push_back(w);
-        by_dev[device] = w;
+        __atomic_store_n(&g_by_dev[device], w, __ATOMIC_RELEASE);
     }
-    return by_dev[device];
+    return w;
 }
+
+// kmws_resident_enable is per calling thread: a thread that switched the
+// worker off launches its jobs (the A/B of the worker), others keep it.
+thread_local uint64_t t_off_mask = 0;  // bit d: off for device d on this thread
+bool off_here(int device) { return device >= 0 && device < kMaxDevices && ((t_off_mask >> device) & 1u); }
 
 }  // namespace
 
@@ -432,9 +456,9 @@ ResidentWorker* worker(int device)
 kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
                             const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2)
 {
-    if (n + n2 > (size_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
+    if (n + n2 > (size_t)kResMaxDescs || off_here(device)) return KMWS_ERR_NOT_SUPPORTED;
     ResidentWorker* w = worker(device);
-    if (!w || !w->usable()) return KMWS_ERR_NOT_SUPPORTED;
+    if (!w) return KMWS_ERR_NOT_SUPPORTED;
     ResDesc job[kResMaxDescs];
     uint64_t bytes = 0;
     size_t k = 0;
@@ -447,7 +471,10 @@ kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* d
         bytes += descs2[i].len;
     }
     if (bytes > kResMaxBytes) return KMWS_ERR_NOT_SUPPORTED;
-    return w->run(job, (uint32_t)k);
+    w->lock();
+    const kmws_status st = w->run(job, (uint32_t)k);
+    w->unlock();
+    return st;
 }
 
 }  // namespace kmws
@@ -456,9 +483,9 @@ extern "C" {
 
 kmws_status kmws_resident_enable(int device, int on)
 {
-    kmws::ResidentWorker* w = kmws::worker(device);
-    if (!w) return KMWS_ERR_INVALID_PARAM;
-    w->set_enabled(on != 0);
+    if (device < 0 || device >= kmws::kMaxDevices) return KMWS_ERR_INVALID_PARAM;
+    if (on) kmws::t_off_mask &= ~(1ull << device);
+    else kmws::t_off_mask |= 1ull << device;
     return KMWS_OK;
 }
 
@@ -466,9 +493,11 @@ kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, i
 {
     kmws::ResidentWorker* w = kmws::worker(device);
     if (!w) return KMWS_ERR_INVALID_PARAM;
+    w->lock();
     if (jobs) *jobs = w->jobs();
     if (launches) *launches = w->launches();
     if (running) *running = w->running();
+    w->unlock();
     return KMWS_OK;
 }
 

@@ -324,7 +324,7 @@ class WSHandler:
 
 
 def resident_info(device: int = 0) -> dict:
-    """kmws_resident_info of the calling thread's resident worker."""
+    """kmws_resident_info of the device's resident worker (shared by the process's threads)."""
     jobs, launches, running = C.c_uint64(0), C.c_uint64(0), C.c_int(0)
     _check(lib().kmws_resident_info(device, C.byref(jobs), C.byref(launches), C.byref(running)),
            "kmws_resident_info")
