@@ -171,3 +171,34 @@ def test_sync_cfg1_resident_drop_in(tmp_path):
     assert all(x["verified"] for x in rows)
     assert {(x["case"], x["codec"]) for x in rows} >= {("decode_sync", "kmws_resident"), ("decode_sync", "kmws_launch"),
                                                        ("mask_sync", "kmws_resident")}
+
+
+def _build_rx_flush(tmp_path):
+    """tests/cpp/rx_flush_bench.cpp: one loop iteration's receive batch timed
+    alone (flush on the resident worker, submit + poll, worker off)."""
+    lib = kb.build()
+    exe = tmp_path / "rx_flush_bench"
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "rx_flush_bench.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-lpthread",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-o", str(exe)])
+    return exe
+
+
+def test_rx_flush_bench_builds(tmp_path):
+    assert _build_rx_flush(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_rx_flush_bench_every_mode_exact(tmp_path):
+    """Every mode delivers every frame unmasked (the program exits non-zero on
+    a wrong byte); small jobs go to the resident worker, the switched-off mode
+    adds no worker job."""
+    import json
+    r = subprocess.run([str(_build_rx_flush(tmp_path)), "200", "4", "4096"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert [x["mode"] for x in rows] == ["flush", "submitpoll", "noresident", "flush", "submitpoll"]
+    assert all(x["bad"] == 0 and x["delivered"] == 250 * 4 for x in rows)
+    assert rows[0]["resident_jobs"] >= 250 and rows[2]["resident_jobs"] == rows[1]["resident_jobs"]
