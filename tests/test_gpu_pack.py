@@ -38,6 +38,13 @@ def frames(rng, kind, n):
         lens = np.full(n, 4096)
     elif kind == "max":  # the decoder's cap WS_MAX_FRAME_DATA_LENGTH (WSHandler.cpp:110) and neighbours
         lens = np.resize(np.array([10485760, 3, 10485759, 0, 10485760 - 13, 10485760]), n)
+    elif kind == "chat":  # a small mean (the chunk form) with large frames (interior chunks) and a
+        # run of tiny ones (chunks of more than 64 frames: the dense kernel)
+        cat = rng.choice(3, size=n, p=[0.6, 0.25, 0.15])
+        lens = np.where(cat == 0, rng.integers(0, 301, size=n),
+                        np.where(cat == 1, rng.integers(0, 9, size=n), rng.integers(4096, 150000, size=n)))
+        run = rng.integers(0, max(1, n - 200))
+        lens[run:run + 200] = rng.integers(0, 6, size=min(200, n - run))
     else:
         raise ValueError(kind)
     fin = rng.integers(0, 2, size=n)
@@ -88,14 +95,14 @@ def gpu_encode(T, src, offs, lens, flags, keys, cap=None):
     return dst.cpu().numpy(), wire_off.cpu().numpy(), ws.status(), total
 
 
-@pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k", "max"])
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "large", "tiny", "frag4k", "max", "chat"])
 @pytest.mark.parametrize("aligned", [True, False])
 @pytest.mark.parametrize("room", [0, 20000])
 def test_encode_parity(T, kind, aligned, room):
     """room = spare output capacity per frame (an output buffer larger than
     the wire: nothing past the wire may be written)."""
     rng = np.random.default_rng(zlib.crc32(f"{kind}-{aligned}".encode()))
-    n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6}[kind]
+    n = {"mixed": 300, "zipf": 200, "large": 40, "tiny": 6000, "frag4k": 320, "max": 6, "chat": 900}[kind]
     lens, flags, keys = frames(rng, kind, n)
     src, offs = src_arena(rng, lens, aligned)
     want, want_off = orc.encode_batch(src, offs, lens, flags, keys)
@@ -130,7 +137,7 @@ def wire_and_offsets(rng, kind, n, mode_mask=1):
     return wire, wire_off, src, offs, lens, flags, keys
 
 
-@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max"])
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max", "chat"])
 @pytest.mark.parametrize("room", [0, 20000])
 def test_unpack_gather_roundtrip(T, kind, room):
     """room = spare arena capacity per frame: 20000 puts the mean region bound
@@ -189,7 +196,7 @@ def test_unpack_gather_roundtrip(T, kind, room):
     assert b"".join(bytes(w2[int(o):int(o) + int(L)]) for o, L in zip(dd["off"], dd["len"])) == orig
 
 
-@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max", "large"])
+@pytest.mark.parametrize("kind", ["mixed", "zipf", "frag4k", "tiny", "max", "large", "chat"])
 def test_fused_unpack_unmask_and_gather_equal_the_two_step_forms(T, kind):
     """kmws_unpack_unmask (header parse writing the unmask plan
     in one kernel, then the in-place unmask) and kmws_unpack_gather (header
