@@ -1000,33 +1000,17 @@ constexpr uint32_t kChunkFrames = 64;           // a chunk's frame table, one la
 
 __host__ __device__ __forceinline__ uint64_t chunk_count(uint64_t bytes) { return (bytes + kChunkBytes - 1) / kChunkBytes; }
 
-// A chunk's record (16 B, one scalar load): the frame holding its first byte,
-// and -- when the whole chunk lies inside that frame's payload (every chunk of
-// a large frame but its first and last) -- the source byte of its first output
-// byte (bit 63 set) and the rotated key: such a chunk is copied with no frame
-// table, no search and no boundary word.
-struct ChunkRec {
-    uint32_t f;      // frame holding the chunk's first byte
-    uint32_t rk;     // interior: rot_key(key, p0) (0: no mask)
-    uint64_t sbase;  // interior: source byte of the chunk's first output byte | 1 << 63; else 0
-};
-static_assert(sizeof(ChunkRec) == 16, "ChunkRec is one 16-byte load");
-constexpr uint64_t kRecInterior = 1ull << 63;
-
 // 256 frames per block, after the scan: each frame's region offset (start[f])
-// and, for every chunk whose first byte lies in the block's regions, its
-// record.  Also the capacity check (status set, nothing stored).
+// and, for every chunk whose first byte lies in the block's regions, the frame
+// holding it (cmap[c]).  Also the capacity check (status set, nothing stored).
 template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) chunk_map_kernel(const uint8_t* __restrict__ src,
-                                                           const kmws_desc* __restrict__ d,
+__global__ void __launch_bounds__(kBlock) chunk_map_kernel(const kmws_desc* __restrict__ d,
                                                            const uint16_t* __restrict__ flags, uint32_t n, uint64_t cap,
                                                            WsHead* __restrict__ head, const V2* __restrict__ tiles,
                                                            uint32_t ntiles, const V2* __restrict__ grp,
-                                                           uint64_t* __restrict__ start, ChunkRec* __restrict__ crec)
+                                                           uint64_t* __restrict__ start, uint32_t* __restrict__ cmap)
 {
     __shared__ uint64_t s_r0[kBlock + 1];
-    __shared__ kmws_desc s_d[kBlock];
-    __shared__ uint8_t s_hl[kBlock];
     __shared__ V2 s_w[kBlock / 64];
     const uint32_t t = threadIdx.x;
     const uint64_t F0 = (uint64_t)blockIdx.x * kBlock;
@@ -1044,10 +1028,6 @@ __global__ void __launch_bounds__(kBlock) chunk_map_kernel(const uint8_t* __rest
     if (t < nf) {
         start[f] = r0;
         s_r0[t] = r0;
-        kmws_desc e = x;
-        if (HEADERS && !((fl >> 8) & 1u)) e.key = 0;  // an unmasked frame
-        s_d[t] = e;
-        s_hl[t] = (uint8_t)(HEADERS ? hdr_len(x.len, (fl >> 8) & 1u) : 0u);
     }
     if (t == 0) s_r0[nf] = pre.a + row.a;
     if (tot.a > cap) {  // block-uniform; the copy waves see the status and store nothing
@@ -1063,17 +1043,7 @@ __global__ void __launch_bounds__(kBlock) chunk_map_kernel(const uint8_t* __rest
             const uint32_t mid = (lo + hi) >> 1;
             if (s_r0[mid] <= xb) lo = mid; else hi = mid;
         }
-        const kmws_desc e = s_d[lo];
-        const uint64_t p0 = s_r0[lo] + s_hl[lo], r1 = p0 + e.len;
-        ChunkRec r;
-        r.f = (uint32_t)F0 + lo;
-        r.rk = 0;
-        r.sbase = 0;
-        if (xb >= p0 && xb + kChunkBytes <= r1 && xb + kChunkBytes <= tot.a) {
-            r.rk = e.key ? rot_key(e.key, p0) : 0u;
-            r.sbase = ((uint64_t)(uintptr_t)src + e.off + (xb - p0)) | kRecInterior;
-        }
-        crec[c] = r;
+        cmap[c] = (uint32_t)F0 + lo;
     }
 }
 
@@ -1138,7 +1108,7 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
                                                             const kmws_desc* __restrict__ d,
                                                             const uint16_t* __restrict__ flags, uint32_t n,
                                                             const uint64_t* __restrict__ start,
-                                                            const ChunkRec* __restrict__ crec,
+                                                            const uint32_t* __restrict__ cmap,
                                                             const V2* __restrict__ tot, WsHead* __restrict__ head,
                                                             uint32_t* __restrict__ dense, uint64_t chunk_base,
                                                             uint32_t split)
@@ -1158,33 +1128,10 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
     const uint32_t st = head->status;
     const uint64_t nch = chunk_count(total);
     if (c >= nch || (st & kStatusBadDesc)) return;  // wave-uniform
-    const uint64_t A0 = c * kChunkBytes;
-    const ChunkRec rec = crec[c];
-    if (rec.sbase & kRecInterior) {  // inside one payload: a shifted, masked copy
-        const uint64_t sb = rec.sbase & ~kRecInterior;
-        const uint32_t delta = (uint32_t)(sb & 15u);
-        const uint8_t* s0 = reinterpret_cast<const uint8_t*>(sb & ~15ull);
-        u32x4 L[kChunkW];
-#pragma unroll
-        for (int i = 0; i < (int)kChunkW; ++i) L[i] = copy_src_load<NT>(s0 + 16u * (64u * i + lane));
-        // the word after the chunk's last source word (the last output word's
-        // second half when the source is shifted; inside the payload)
-        uint32_t xk = delta ? kChunkWords : 0u;
-        asm("" : "+v"(xk));  // a vector load, like the others
-        const u32x4 X = copy_src_load<NT>(s0 + 16u * xk);
-#pragma unroll
-        for (int i = 0; i < (int)kChunkW; ++i) {
-            u32x4 hi = shfl16_down1(L[i]);
-            const u32x4 nx = i + 1 < (int)kChunkW ? readlane0(L[i + 1 < (int)kChunkW ? i + 1 : i]) : X;
-            if (lane == 63) hi = nx;
-            const u32x4 out = funnel16(L[i], hi, delta) ^ rec.rk;
-            __builtin_nontemporal_store(out, reinterpret_cast<u32x4*>(dst + A0 + 16ull * (64u * i + lane)));
-        }
-        return;
-    }
-    const uint32_t f0 = rec.f;
-    const uint32_t f1 = c + 1 < nch ? crec[c + 1].f : n - 1;  // holds the next chunk's first byte
+    const uint32_t f0 = cmap[c];
+    const uint32_t f1 = c + 1 < nch ? cmap[c + 1] : n - 1;  // holds the next chunk's first byte
     const uint32_t nfr = f1 - f0 + 1;
+    const uint64_t A0 = c * kChunkBytes;
     if (nfr > kChunkFrames) {
         if (lane == 0) dense[atomicAdd(&head->pad[0], 1u)] = (uint32_t)c;
         return;
@@ -1354,7 +1301,7 @@ __global__ void __launch_bounds__(kBlock) chunk_dense_kernel(const uint8_t* __re
                                                              const kmws_desc* __restrict__ d,
                                                              const uint16_t* __restrict__ flags, uint32_t n,
                                                              const uint64_t* __restrict__ start,
-                                                             const ChunkRec* __restrict__ crec,
+                                                             const uint32_t* __restrict__ cmap,
                                                              const V2* __restrict__ tot,
                                                              const WsHead* __restrict__ head,
                                                              const uint32_t* __restrict__ dense)
@@ -1366,7 +1313,7 @@ __global__ void __launch_bounds__(kBlock) chunk_dense_kernel(const uint8_t* __re
     const uint32_t nw = gridDim.x * (kBlock / 64);
     for (uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < cnt; i += nw) {
         const uint64_t c = dense[i];
-        const uint32_t f0 = crec[c].f, f1 = c + 1 < nch ? crec[c + 1].f : n - 1;
+        const uint32_t f0 = cmap[c], f1 = c + 1 < nch ? cmap[c + 1] : n - 1;
         for (uint32_t k = lane; k < kChunkWords; k += 64) {
             const uint64_t a = c * kChunkBytes + 16ull * k;
             if (a >= total) break;
@@ -1870,7 +1817,7 @@ struct CopyWs {
     V2* grp;    // one per 256-frame row: its prefix inside the tile
     UnitRec* rec;
     u32x4* edge;
-    ChunkRec* crec;   // per output chunk: its first frame, and the interior copy's source
+    uint32_t* cmap;   // chunk -> frame holding its first byte
     uint32_t* dense;  // chunks chunk_copy_kernel left to chunk_dense_kernel
 };
 
@@ -1903,7 +1850,7 @@ static size_t copy_ws_size(uint32_t n, uint64_t cap)
 {
     if (!use_chunks(n, cap))
         return r256(scan_ws_size(n)) + r256((uint64_t)n * kEdgeWords * 16) + max_units(n, cap) * sizeof(UnitRec);
-    return r256(scan_ws_size(n)) + r256((chunk_count(cap) + 1) * sizeof(ChunkRec)) +
+    return r256(scan_ws_size(n)) + r256((chunk_count(cap) + 1) * sizeof(uint32_t)) +
            r256(chunk_count(cap) * sizeof(uint32_t));
 }
 
@@ -1914,8 +1861,8 @@ static bool carve(void* ws, size_t ws_bytes, uint32_t n, uint64_t cap, CopyWs& c
     carve_scan(p, n, c);
     p += r256(scan_ws_size(n));  // edge words and records (or the chunk map) on whole lines
     c.edge = reinterpret_cast<u32x4*>(p);
-    c.crec = reinterpret_cast<ChunkRec*>(p);
-    c.dense = reinterpret_cast<uint32_t*>(p + r256((chunk_count(cap) + 1) * sizeof(ChunkRec)));
+    c.cmap = reinterpret_cast<uint32_t*>(p);
+    c.dense = c.cmap + r256((chunk_count(cap) + 1) * sizeof(uint32_t)) / sizeof(uint32_t);
     p += r256((uint64_t)n * kEdgeWords * 16);
     c.rec = reinterpret_cast<UnitRec*>(p);
     return true;
@@ -1963,8 +1910,8 @@ template <bool HEADERS>
 static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
                                  const uint16_t* flags, uint32_t n, CopyWs& c, uint32_t nt, hipStream_t s)
 {
-    hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
-                       c.head, c.tiles, nt, c.grp, start, c.crec);
+    hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, d, flags, n, cap,
+                       c.head, c.tiles, nt, c.grp, start, c.cmap);
     const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
     constexpr uint64_t kWaves = kBlock / 64;
     constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
@@ -1976,14 +1923,14 @@ static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap,
         const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
         if (nt_loads)
             hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags, n,
-                               start, c.crec, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
+                               start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
         else
             hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
-                               n, start, c.crec, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
+                               n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
     }
     const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
     hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n, start,
-                       c.crec, c.tiles + nt, c.head, c.dense);
+                       c.cmap, c.tiles + nt, c.head, c.dense);
     return hip_status(hipGetLastError());
 }
 
