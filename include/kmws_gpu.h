@@ -303,7 +303,10 @@ kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* 
 /* ---- batched header pack / unpack (device) ---- */
 
 /* Workspace bytes for kmws_encode_batch / kmws_gather_unmask with n frames
- * and an output capacity of dst_cap bytes. */
+ * and an output capacity of dst_cap bytes.  The copy form follows dst_cap / n
+ * (below 16 KiB per frame: 4 KiB output chunks, one wave each, 8 B of
+ * workspace per chunk; from it: per-frame edge words and 32 B per 4 KiB
+ * output unit), so size the workspace with the dst_cap the call will pass. */
 size_t kmws_copy_workspace_size(uint32_t n, uint64_t dst_cap);
 
 /* Batched frame encode: for frame i, WSHandler::encodeFrameHeader
