@@ -104,14 +104,13 @@ constexpr int kResMaxDescs = 128;
 // One workgroup moves a job over PCIe at ~3 GB/s: at 64 KiB it is as fast as a
 // launch of the multi-block pieces kernel (20 us each, tests/cpp/rx_flush_bench.cpp,
 // profiles/r04w_rx_flush_bench.jsonl), below it faster (10.7 vs 18.5 us at 16
-// KiB), above it slower (the loopback cfg1 receive loop flushing 64-256 KiB
-// ran at 0.9-1.0 GiB/s on the worker against 2.0 launched, r04x).
+// KiB); above it the launch's several blocks move the bytes faster.
 constexpr uint64_t kResMaxBytes = 64u << 10;
 // Unmasks descs[0..n) over dev_base and descs2[0..n2) over dev_base2 (device
 // views of pinned host memory, offsets relative to them), synchronously.
-// KMWS_ERR_NOT_SUPPORTED: too large for one job, or no worker on this thread
-// and device -- the caller launches instead.  Any other error: the job may or
-// may not have run.
+// KMWS_ERR_NOT_SUPPORTED: too large for one job, the calling thread switched
+// the worker off, or it is unusable -- the caller launches instead.  Any other
+// error: the job may or may not have run.
 kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
                             const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2);
 

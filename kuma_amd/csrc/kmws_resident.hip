@@ -451,8 +451,10 @@ bool off_here(int device) { return device >= 0 && device < kMaxDevices && ((t_of
 }  // namespace
 
 // Synchronous unmask of host payloads (device-visible views of pinned memory)
-// through this thread's resident worker.  KMWS_ERR_NOT_SUPPORTED: the job does
-// not fit a worker job (or the worker is off / unusable); the caller launches.
+// through the device's resident worker.  KMWS_ERR_NOT_SUPPORTED: the job does
+// not fit a worker job (more than kResMaxDescs payloads or kResMaxBytes bytes),
+// the calling thread switched the worker off, or it is unusable; the caller
+// launches.
 kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
                             const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2)
 {
