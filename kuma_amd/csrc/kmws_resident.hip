@@ -93,7 +93,13 @@ static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 // job's tag, and the job's descriptors are then read again after the word.
 constexpr uint64_t kJobMask = (1ull << 40) - 1;
 constexpr uint64_t kQuitBit = 1ull << 63;
-constexpr int kPollDescs = 15;  // word + 15 slots: the mailbox's first 256 bytes
+// word + 31 slots: the mailbox's first 512 bytes, one 16-byte load per lane
+// of wave 0 -- a cfg1 read (16 frames of 4 KiB, and a partial one) fits
+#ifndef KMWS_RESIDENT_POLL_DESCS
+#define KMWS_RESIDENT_POLL_DESCS 31
+#endif
+constexpr int kPollDescs = KMWS_RESIDENT_POLL_DESCS;
+static_assert(kPollDescs < 64, "one lane of wave 0 per polled slot");
 constexpr uint64_t kAddrMask = (1ull << 48) - 1;
 constexpr uint32_t kLenMask = (1u << 21) - 1;  // kResMaxBytes fits
 static_assert(kResMaxBytes <= kLenMask, "tagged length");
