@@ -525,7 +525,8 @@ __device__ uint64_t g_trace_pro[(1u << 16) * 8];
 #else
 #define KMWS_TRACE_PRO(ev) do { } while (0)
 #endif
-// The prologue's per-row part, shared by prologue_kernel and pack_rows_kernel:
+// The prologue's per-row part (prologue_kernel; round 4's rejected fused row
+// kernel shared it, profiles/r04i_pack_rows_ab.txt):
 // row `row`'s frame offsets (written to start[]), its frames' unit geometry
 // (s_fu, unit slot bases s_ub relative to the row's first slot) and edge words
 // (s_edge, live counts s_ne), all in LDS.  Returns false (block-uniform) when
@@ -816,7 +817,7 @@ struct UnitRegs {
 // interior word from `ex`.  Edge words (composed by edge_block: [klo, ilo)
 // then [ihi, khi)): one per lane, index clamped.
 // fedge: the owning frame's kEdgeWords edge words (global: edge + f * kEdgeWords,
-// or the row's LDS copy in pack_rows_kernel).
+// or an LDS copy of them).
 __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const uint8_t* __restrict__ src,
                                            const u32x4* __restrict__ fedge, UnitRegs& R)
 {
@@ -952,17 +953,6 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const uint8_t* __restrict_
     UnitRegs R;
     unit_issue(x, lane, src, edge + (uint64_t)x.f * kEdgeWords, R);
     unit_finish(x, lane, dst, total, R);
-}
-
-// A wave-uniform 64-bit value into scalar registers.  readfirstlane returns a
-// signed int: each half goes through uint32_t, or a low half with bit 31 set
-// would sign-extend over the high half (an output offset past 2 GiB became an
-// address near 2^64 -- an illegal access, caught by tools/diag_pack_rows.py).
-__device__ __forceinline__ uint64_t uniform64(uint64_t v)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return (uint64_t)hi << 32 | lo;
 }
 
 __device__ __forceinline__ u32x4 shfl16_down1(const u32x4& v)
@@ -1332,104 +1322,6 @@ __global__ void __launch_bounds__(kBlock) chunk_dense_kernel(const uint8_t* __re
             else store_word_bytes(dst, a, total, v);
         }
     }
-}
-
-#ifndef KMWS_PACK_ROWS_PIPE
-#define KMWS_PACK_ROWS_PIPE 1  // two units in flight per wave (0: one; A/B builds)
-#endif
-
-// Small-frame batches, a measured and rejected design (tuning builds only,
-// KMWS_PACK_ROWS_MAX_MEAN): the prologue and the copy of one
-// 256-frame row in ONE block.  The row's unit geometry and edge words stay in
-// LDS and the block's own waves copy the row's units (wave w takes slots w,
-// w + 4, ...; a frame cursor per wave, no search), so the edge-word buffer
-// and the unit records never go through HBM (write + read: 2 x (80 + 32 x
-// units) bytes per frame, ~5 % of a 4 KiB fragment), there is no kernel
-// boundary between the two, and a row's boundary source lines are read by one
-// CU.  Load balance is a row's: batches of large frames keep the two-kernel
-// form (launch_copy_tail).  A bad batch (output over cap) stores nothing:
-// every block sees the same total before its first store.  Measured on cfg4
-// (4 M x 4 KiB): HBM traffic 1.028 x algorithmic (the two-kernel form: 1.057
-// x) but 0.64 of peak against 0.72 -- 34 KiB of LDS per block holds 4 blocks
-// (16 waves) per CU against the copy grid's 32 waves, and a row's 512 units
-// are four waves' serial work; two units in flight per wave did not change it.
-template <bool HEADERS>
-__global__ void __launch_bounds__(kBlock) pack_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                           const kmws_desc* __restrict__ d,
-                                                           const uint16_t* __restrict__ flags, uint32_t n,
-                                                           uint64_t cap, WsHead* __restrict__ head,
-                                                           const V2* __restrict__ tiles, uint32_t ntiles,
-                                                           const V2* __restrict__ grp, uint64_t* __restrict__ start)
-{
-    __shared__ RowLds L;
-    RowInfo ri;
-    if (!row_prologue<HEADERS>(blockIdx.x, src, d, flags, n, cap, head, tiles, ntiles, grp, start, L, ri)) return;
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nf = ri.nf, ns = L.ub[nf];
-    const uint64_t total = ri.total;
-    uint32_t cur = 0;  // frame of the wave's current slot (slots ascend)
-#if KMWS_PACK_ROWS_PIPE
-    // Two units in flight per wave: the next unit's loads are issued before the
-    // current unit is composed and stored (its wait then counts only the loads
-    // issued before the stores of the unit before it).
-    uint32_t sl = wave;
-    auto next = [&](UnitInfo& x, uint32_t& e) -> bool {
-        for (; sl < ns; sl += kBlock / 64) {
-            while (cur + 1 < nf && L.ub[cur + 1] <= sl) ++cur;
-            cur = __builtin_amdgcn_readfirstlane(cur);
-            const uint32_t m = sl - L.ub[cur];
-            const FrameUnits fu = L.fu[cur];
-            if (m >= fu.units) continue;
-            UnitRec r = make_rec(fu, m, (uint32_t)ri.F0 + cur, head);
-            r.dst = uniform64(r.dst);
-            r.src = uniform64(r.src);
-            r.rk = __builtin_amdgcn_readfirstlane(r.rk);
-            r.own = __builtin_amdgcn_readfirstlane(r.own);
-            r.inner = __builtin_amdgcn_readfirstlane(r.inner);
-            x = decode_unit(r, true, src);
-            if (x.khi == 0) continue;
-            e = cur * kEdgeWords;
-            sl += kBlock / 64;
-            return true;
-        }
-        return false;
-    };
-    UnitInfo xa, xb;
-    UnitRegs Ra, Rb;
-    uint32_t ea = 0, eb = 0;
-    if (!next(xa, ea)) return;
-    unit_issue(xa, lane, src, L.edge + ea, Ra);
-    for (;;) {
-        const bool hb = next(xb, eb);
-        if (hb) unit_issue(xb, lane, src, L.edge + eb, Rb);
-        unit_finish(xa, lane, dst, total, Ra);
-        if (!hb) break;
-        const bool ha = next(xa, ea);
-        if (ha) unit_issue(xa, lane, src, L.edge + ea, Ra);
-        unit_finish(xb, lane, dst, total, Rb);
-        if (!ha) break;
-    }
-#else
-    for (uint32_t sl = wave; sl < ns; sl += kBlock / 64) {
-        while (cur + 1 < nf && L.ub[cur + 1] <= sl) ++cur;
-        cur = __builtin_amdgcn_readfirstlane(cur);
-        const uint32_t m = sl - L.ub[cur];
-        const FrameUnits fu = L.fu[cur];
-        if (m >= fu.units) continue;  // slots past a frame's exact unit count
-        UnitRec r = make_rec(fu, m, (uint32_t)ri.F0 + cur, head);
-        r.dst = uniform64(r.dst);
-        r.src = uniform64(r.src);
-        r.rk = __builtin_amdgcn_readfirstlane(r.rk);
-        r.own = __builtin_amdgcn_readfirstlane(r.own);
-        r.inner = __builtin_amdgcn_readfirstlane(r.inner);
-        const UnitInfo x = decode_unit(r, true, src);
-        if (x.khi == 0) continue;
-        UnitRegs R;
-        unit_issue(x, lane, src, L.edge + cur * kEdgeWords, R);
-        unit_finish(x, lane, dst, total, R);
-    }
-#endif
 }
 
 // ------------------------------ header unpack / validate ------------------------------
@@ -1902,11 +1794,6 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
     return launch_copy_tail<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
 }
 
-// The prologue and the copy grid, after the scan.  A tuning build
-// (KMWS_PACK_ROWS_MAX_MEAN = a mean-region bound in bytes; cap / n bounds the
-// mean from above) runs batches of small frames through the fused row kernel
-// instead: measured slower on cfg4 (0.64 vs 0.72 of HBM peak,
-// profiles/r04i_pack_rows_ab.txt), so the product never does.
 // The chunk form after the scan: chunk_map, the chunk copy grid, the dense
 // chunks (usually none: the grid of chunk_dense_kernel exits at once).
 template <bool HEADERS>
@@ -1937,22 +1824,14 @@ static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap,
     return hip_status(hipGetLastError());
 }
 
-#ifndef KMWS_PACK_ROWS_MAX_MEAN
-#define KMWS_PACK_ROWS_MAX_MEAN 0
-#endif
+// The copy form after the scan: chunks (small mean) or the prologue and the
+// unit copy grid.
 template <bool HEADERS>
 static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
 {
     const uint32_t nt = (uint32_t)n_tiles(n);
     if (use_chunks(n, cap)) return launch_chunks<HEADERS>(src, dst, cap, start, d, flags, n, c, nt, s);
-#if KMWS_PACK_ROWS_MAX_MEAN > 0
-    if (cap / n <= (uint64_t)KMWS_PACK_ROWS_MAX_MEAN) {
-        hipLaunchKernelGGL(pack_rows_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, dst, d, flags,
-                           n, cap, c.head, c.tiles, nt, c.grp, start);
-        return hip_status(hipGetLastError());
-    }
-#endif
     hipLaunchKernelGGL(prologue_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, src, d, flags, n, cap,
                        c.head, c.tiles, nt, c.grp, start, c.rec, c.edge);
     // Occupancy: runs of large frames stream faster with 5 blocks per CU (fewer
