@@ -191,3 +191,21 @@ def test_batch_entries_reject_bad_arguments_before_any_device_work():
     assert L.kmws_find_headers_streams(fake, 64, None, 3, fake, 4, fake, None, None) == kmws.ERR_INVALID_PARAM
     assert L.kmws_find_headers_streams(fake, 64, fake, 3, None, 4, fake, None, None) == kmws.ERR_INVALID_PARAM
     assert L.kmws_find_headers_streams(None, 0, None, 0, None, 0, None, None, None) == 0  # nothing to do
+
+
+def test_copy_workspace_size_follows_the_copy_form():
+    """kmws_copy_workspace_size (no device needed): below a 16 KiB mean region
+    bound (dst_cap / n) the chunk form's 8 B per 4 KiB output chunk, from it the
+    unit form's edge words (80 B per frame) and 32-byte unit records -- so the
+    same (n, dst_cap) the call passes must size the workspace."""
+    n = 1000
+    small = kmws.copy_workspace_size(n, n * 4104)        # cfg4-like: chunk form
+    large = kmws.copy_workspace_size(n, n * 65550)       # 64 KiB frames: unit form
+    chunks = -(-n * 4104 // 4096)
+    assert small >= 8 * chunks and small < 8 * chunks + 64 * 1024
+    assert large >= 80 * n + 32 * (n * 65550 // 4096)
+    # the threshold: dst_cap / n crosses 16 KiB
+    below = kmws.copy_workspace_size(n, n * 16383)
+    above = kmws.copy_workspace_size(n, n * 16384)
+    assert above > below + 80 * n // 2
+    assert kmws.copy_workspace_size(0, 0) > 0
