@@ -1580,6 +1580,106 @@ __global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict
         p[i] = 0;
 }
 
+// The chunk form's front in ONE pass (KMWS_CHUNK_ONE_PASS, the default): a 2048-frame
+// tile per block, the scan by decoupled look-back (the header-only pack's
+// machinery above), then the tile's region offsets and its chunks' first
+// frames -- in place of reduce_kernel + scan_tiles_kernel + chunk_map_kernel,
+// which read the descriptors twice.  The tile states, the status word and the
+// dense count are zeroed by the launch before it.  The last tile writes the
+// total (start[n] and tot) and the capacity check; every tile clips its chunk
+// map to the capacity, so an oversized batch writes nothing out of bounds.
+template <bool HEADERS>
+__global__ void __launch_bounds__(kBlock) chunk_scan_kernel(const kmws_desc* __restrict__ d,
+                                                            const uint16_t* __restrict__ flags, uint32_t n,
+                                                            uint64_t cap, WsHead* __restrict__ head,
+                                                            uint64_t* __restrict__ st, V2* __restrict__ tot,
+                                                            uint64_t* __restrict__ start, uint32_t* __restrict__ cmap)
+{
+    __shared__ uint64_t s_sz[kScanTile];  // region sizes, then offsets
+    __shared__ uint64_t s_w[kBlock / 64];
+    __shared__ uint64_t s_a[kBlock / 64];
+    __shared__ uint64_t s_pre;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t F = (uint64_t)tile * kScanTile;
+    uint32_t len[kScanItems], fl[kScanItems];
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        const uint32_t j = (uint32_t)__builtin_elementwise_min(f, (uint64_t)n - 1);
+        len[i] = d[j].len;
+        fl[i] = HEADERS ? flags[j] : 0u;
+    }
+    uint64_t part = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        const uint64_t r = (uint64_t)(HEADERS ? hdr_len(len[i], (fl[i] >> 8) & 1u) : 0u) + len[i];
+        part += f < n ? r : 0;
+        s_sz[i * kBlock + t] = f < n ? r : 0;
+    }
+    part = wave_sum(part);
+    if (lane == 0) s_a[wave] = part;
+    lds_barrier();
+    uint64_t agg = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) agg += s_a[w];
+    if (t == 0) st_agent(st + tile, tile == 0 ? agg << 2 | kStInc : agg << 2 | kStAgg);
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) sum += s_sz[kScanItems * t + k];
+    const uint64_t inc = wave_incl_scan(sum);
+    if (lane == 63) s_w[wave] = inc;
+    lds_barrier();
+    uint64_t before = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w)
+        if (w < (int)wave) before += s_w[w];
+    uint64_t pre = 0;
+    if (tile != 0) {
+        if (wave == 0) {
+            const uint64_t p = look_back(st, tile, head);
+            if (lane == 0) s_pre = p;
+        }
+        lds_barrier();
+        pre = s_pre;
+        if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
+    }
+    uint64_t run = pre + before + inc - sum;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t r = s_sz[kScanItems * t + k];
+        s_sz[kScanItems * t + k] = run;
+        run += r;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t f = F + (uint64_t)i * kBlock + t;
+        if (f < n) start[f] = s_sz[i * kBlock + t];
+    }
+    const uint64_t T0 = pre, T1 = pre + agg;
+    if (t == 0 && F + kScanTile >= n) {  // the last tile: the total and the capacity check
+        start[n] = T1;
+        tot->a = T1;
+        tot->b = 0;
+        if (T1 > cap) atomicOr(&head->status, kStatusBadDesc);
+    }
+    const uint32_t nf = n - F < (uint64_t)kScanTile ? (uint32_t)(n - F) : (uint32_t)kScanTile;
+    const uint64_t cap_chunks = chunk_count(cap);
+    uint64_t c1 = chunk_count(T1);
+    c1 = c1 < cap_chunks ? c1 : cap_chunks;
+    for (uint64_t c = chunk_count(T0) + t; c < c1; c += kBlock) {
+        const uint64_t xb = c * kChunkBytes;
+        uint32_t lo = 0, hi = nf;  // s_sz[lo] <= xb < s_sz[hi] (s_sz[nf] stands for T1)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_sz[mid] <= xb) lo = mid; else hi = mid;
+        }
+        cmap[c] = (uint32_t)(F + lo);
+    }
+}
+
 // ------------------------------ header-chain walk, many streams ------------------------------
 // One lane per stream, the rules of kmws_find_headers (kmws_codec.cpp) /
 // the header states of WSHandler::decodeFrame (WSHandler.cpp:118-197): each
@@ -1780,6 +1880,17 @@ template <bool HEADERS>
 static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s);
 
+// The chunk form's front: one look-back pass (chunk_scan_kernel; 1) or reduce +
+// scan + chunk_map (0).  Same box (profiles/r04aq_chunk_one_pass_ab.txt): cfg4
+// 0.752-0.767 / 0.774-0.779 against 0.749-0.766 / 0.772-0.777, 1-300 B frames
+// 0.35-0.40 / 0.45-0.49 against 0.34-0.39 / 0.44-0.48 (encode / gather).
+#ifndef KMWS_CHUNK_ONE_PASS
+#define KMWS_CHUNK_ONE_PASS 1
+#endif
+template <bool HEADERS>
+static kmws_status launch_chunks_one_pass(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                          const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c,
+                                          hipStream_t s);
 template <bool HEADERS>
 static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
                                const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s)
@@ -1788,6 +1899,9 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
         if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
         return launch_zero(start, sizeof(uint64_t), s);
     }
+#if KMWS_CHUNK_ONE_PASS
+    if (use_chunks(n, cap)) return launch_chunks_one_pass<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
+#endif
     const kmws_status st = HEADERS ? launch_reduce(WireSize{d, flags}, n, start, c, s)
                                    : launch_reduce(PayloadSize{d}, n, start, c, s);
     if (st != KMWS_OK) return st;
@@ -1797,11 +1911,42 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
 // The chunk form after the scan: chunk_map, the chunk copy grid, the dense
 // chunks (usually none: the grid of chunk_dense_kernel exits at once).
 template <bool HEADERS>
+static kmws_status launch_chunk_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, uint32_t nt,
+                                     hipStream_t s);
+template <bool HEADERS>
 static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start, const kmws_desc* d,
                                  const uint16_t* flags, uint32_t n, CopyWs& c, uint32_t nt, hipStream_t s)
 {
     hipLaunchKernelGGL(chunk_map_kernel<HEADERS>, dim3((uint32_t)n_rows(n)), dim3(kBlock), 0, s, d, flags, n, cap,
                        c.head, c.tiles, nt, c.grp, start, c.cmap);
+    return launch_chunk_copy<HEADERS>(src, dst, cap, start, d, flags, n, c, nt, s);
+}
+
+// The chunk form's front in one pass (KMWS_CHUNK_ONE_PASS):
+// zero the head, the totals and the tile states, then chunk_scan_kernel.
+template <bool HEADERS>
+static kmws_status launch_chunks_one_pass(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                          const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c,
+                                          hipStream_t s)
+{
+    const uint32_t nt = (uint32_t)n_tiles(n);
+    // head | tile totals (nt + 1) | the row-prefix area, whose first nt words hold the states
+    const uint64_t words = (r16(sizeof(WsHead)) + (uint64_t)(nt + 1) * sizeof(V2) + (uint64_t)nt * 8) / 8;
+    const uint64_t zb = (words + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(zb < 1024 ? zb : 1024)), dim3(kBlock), 0, s,
+                       reinterpret_cast<uint64_t*>(c.head), words);
+    hipLaunchKernelGGL(chunk_scan_kernel<HEADERS>, dim3(nt), dim3(kBlock), 0, s, d, flags, n, cap, c.head,
+                       reinterpret_cast<uint64_t*>(c.grp), c.tiles + nt, start, c.cmap);
+    return launch_chunk_copy<HEADERS>(src, dst, cap, start, d, flags, n, c, nt, s);
+}
+
+// The chunk copy grid and the dense chunks.
+template <bool HEADERS>
+static kmws_status launch_chunk_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
+                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, uint32_t nt,
+                                     hipStream_t s)
+{
     const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
     constexpr uint64_t kWaves = kBlock / 64;
     constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
