@@ -1117,7 +1117,8 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
     const uint64_t total = tot->a;
     const uint32_t st = head->status;
     const uint64_t nch = chunk_count(total);
-    if (c >= nch || (st & kStatusBadDesc)) return;  // wave-uniform
+    // a bad batch, or offsets from a look-back that timed out: nothing is stored
+    if (c >= nch || (st & (kStatusBadDesc | kStatusLookbackTimeout))) return;  // wave-uniform
     const uint32_t f0 = cmap[c];
     const uint32_t f1 = c + 1 < nch ? cmap[c + 1] : n - 1;  // holds the next chunk's first byte
     const uint32_t nfr = f1 - f0 + 1;
@@ -1299,7 +1300,7 @@ __global__ void __launch_bounds__(kBlock) chunk_dense_kernel(const uint8_t* __re
                                                              const WsHead* __restrict__ head,
                                                              const uint32_t* __restrict__ dense)
 {
-    if (head->status & kStatusBadDesc) return;
+    if (head->status & (kStatusBadDesc | kStatusLookbackTimeout)) return;
     const uint32_t cnt = head->pad[0];
     const uint64_t total = tot->a, nch = chunk_count(total);
     const int lane = threadIdx.x & 63;
