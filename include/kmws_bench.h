@@ -57,16 +57,23 @@ kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t se
                                 const kmws_desc* descs, uint32_t n,
                                 unsigned long long* mismatches, void* stream);
 
-/* The resident worker on `device` (kmws_resident.hip): one per device, shared
- * by the process's threads, which serves the synchronous host entries
- * (kmws_decoder_feed, kmws_mask_host_chain; jobs of <= 128 payloads and
- * <= 64 KiB) without a launch per call.  enable(0) makes the CALLING thread's
- * calls launch a kernel per call instead (the A/B of bench.py cfg1); info: jobs
+/* The resident worker on `device` (kmws_resident.hip): one grid per device of
+ * 16 workgroups, one per mailbox slot; a host thread claims a slot at its first
+ * job and keeps it until it exits, so up to 16 loop threads run their jobs at
+ * once (a thread finding no free slot launches instead).  It serves the host
+ * entries' small jobs (kmws_decoder_feed, kmws_mask_host_chain, rx / tx batch
+ * flushes and submits; <= 128 payloads and <= 64 KiB) without a launch per
+ * call.  enable(0) makes the CALLING thread's calls launch a kernel per call
+ * instead (the A/B of bench.py cfg1) and gives its slot back; info: jobs
  * served, launches (incarnations) so far, and whether it is on the GPU now (it
- * exits 200 us after its last job and after a 1 ms lease; until then a
- * device-wide synchronize such as torch.cuda.synchronize waits for it). */
+ * exits 200 us after the last job of any slot and after a 1 ms lease; until
+ * then a device-wide synchronize such as torch.cuda.synchronize waits for
+ * it); counters: the calling thread's slot (-1: none), slots held, jobs that
+ * hit the timeout, jobs withdrawn unrun (and launched by their caller). */
 kmws_status kmws_resident_enable(int device, int on);
 kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, int* running);
+kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_claimed, uint64_t* timeouts,
+                                   uint64_t* withdrawn);
 
 #ifdef __cplusplus
 }

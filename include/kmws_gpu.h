@@ -40,6 +40,8 @@ extern "C" {
 typedef int kmws_status;
 #define KMWS_OK                    0
 #define KMWS_ERR_FAILED           (-1)   /* KMError::FAILED (HIP runtime error) */
+#define KMWS_ERR_TIMEOUT          (-6)   /* KMError::TIMEOUT: a host job the device neither finished nor
+                                            gave up in time; the device may still write its buffer */
 #define KMWS_ERR_INVALID_STATE    (-7)   /* KMError::INVALID_STATE */
 #define KMWS_ERR_INVALID_PARAM    (-8)   /* KMError::INVALID_PARAM */
 #define KMWS_ERR_BUFFER_TOO_SMALL (-17)  /* KMError::BUFFER_TOO_SMALL */
@@ -294,10 +296,12 @@ int kmws_unmask_autotune(uint8_t* base, uint64_t span, const kmws_desc* descs, u
                          size_t workspace_bytes, void* stream);
 
 /* Read (synchronously) the status word of a workspace after a batch call, a
- * bit set: 0 = OK, 1 = descriptor precondition violated, 2 = header error seen,
- * 4 = the header-pack scan timed out waiting for a predecessor tile's state
- * (kmws_pack_headers: wire_off is then invalid; never seen with in-order
- * workgroup dispatch). */
+ * bit set: 0 = OK, 1 = descriptor precondition violated (or the output would
+ * exceed dst_cap), 2 = header error seen, 4 = a scan timed out waiting for a
+ * predecessor tile's state (kmws_pack_headers, and kmws_encode_batch /
+ * kmws_gather_unmask in their chunk form: never seen with in-order workgroup
+ * dispatch).  The offsets those calls write (wire_off, dst_off) are valid
+ * only when the status is 0; with bit 1 or 4 set nothing is stored in dst. */
 kmws_status kmws_read_status(const void* workspace, uint32_t* status_out, void* stream);
 
 /* ---- batched header pack / unpack (device) ---- */
@@ -315,8 +319,9 @@ size_t kmws_copy_workspace_size(uint32_t n, uint64_t dst_cap);
  * (WebSocketImpl.cpp:381-404), all frames back to back in dst.  wire_off
  * (n+1 entries, device) receives each frame's header offset and, in
  * wire_off[n], the total wire size.  If the total exceeds dst_cap nothing is
- * written and the workspace status word is set.  src and dst 16-B aligned;
- * source payloads may overlap or sit anywhere in src. */
+ * written and the workspace status word is set.  wire_off and dst are valid
+ * only when the status (kmws_read_status) is 0 afterwards.  src and dst 16-B
+ * aligned; source payloads may overlap or sit anywhere in src. */
 kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const uint16_t* flags, uint32_t n,
                               uint8_t* dst, uint64_t dst_cap, uint64_t* wire_off, void* workspace,
                               size_t workspace_bytes, void* stream);
@@ -373,7 +378,8 @@ kmws_status kmws_unpack_unmask(uint8_t* wire, uint64_t wire_len, const uint64_t*
 
 /* Out-of-place unmask: frame i's payload src[descs[i].off .. +len) XOR its key
  * is written densely to dst at dst_off[i] (exclusive scan of len; n+1
- * entries, dst_off[n] = total).  Nothing is written if total > dst_cap. */
+ * entries, dst_off[n] = total).  Nothing is written if total > dst_cap.
+ * dst_off and dst are valid only when the workspace status is 0 afterwards. */
 kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint32_t n, uint8_t* dst,
                                uint64_t dst_cap, uint64_t* dst_off, void* workspace, size_t workspace_bytes,
                                void* stream);

@@ -51,11 +51,15 @@
 #ifndef KMWS_WSHANDLER_HPP
 #define KMWS_WSHANDLER_HPP
 
+#include <sys/uio.h>
+
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
+#include <new>
 #include <utility>
 #include <vector>
 
@@ -144,6 +148,326 @@ private:
     bool armed_ = false;
     int last_ = 0;
     std::shared_ptr<bool> alive_;
+};
+
+// The batched send path of one event-loop thread: WebSocket::Impl::sendWsFrame
+// (WebSocketImpl.cpp:381-436) masks the caller's payload with one
+// handleDataMask per send, packs the header and writes both as one iovec.
+// With a TxLoop, send() packs the header at once and copies the payload into
+// the loop's pinned send ring (the bytes kuma would hand the socket); the
+// loop's posted task (kuma: EventLoop::post, kmapi.h:204-210) masks every
+// payload queued in the iteration with ONE GPU job and writes each
+// connection's frames, in send order, as soon as their generation's mask has
+// completed -- the GPU round trip overlaps the next iteration instead of
+// stalling every send.  At most `max_inflight` generations are in flight (2:
+// the loop fills and submits iteration k while iteration k - 1's masks run);
+// a third waits for the oldest.
+//
+// Differences from sendWsFrame, observable only to the sender:
+//  * the frame reaches the socket at the iteration's task, not before send()
+//    returns; a writer error is reported by Conn::lastResult() / lastResult(),
+//    not by send();
+//  * the caller's payload buffer is not modified (kuma masks it in place,
+//    :388/:414) and may be reused as soon as send() returns;
+//  * an unmasked frame (server mode) whose connection has nothing queued is
+//    written at once, without a copy -- exactly sendWsFrame's path.
+class TxLoop {
+public:
+    using Task = std::function<void()>;
+    using Poster = std::function<void(Task)>;
+    // kuma: [conn](const iovec* v, int n) { return conn->send(v, n); } (negative: error, :432)
+    using Writer = std::function<int(const iovec* iov, int cnt)>;
+
+    // One connection's queue: its frames are written in send order.
+    class Conn {
+    public:
+        int lastResult() const { return last_; }  // the writer's last result (negative: an error)
+        int queued() const { return queued_; }    // frames sent but not yet written
+
+    private:
+        friend class TxLoop;
+        explicit Conn(Writer w) : write_(std::move(w)) {}
+        Writer write_;
+        int queued_ = 0;
+        int last_ = 0;
+    };
+
+    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)16 << 20, int max_inflight = 2)
+        : post_(std::move(post)), batch_(kmws_tx_batch_create(device)), max_inflight_(max_inflight < 1 ? 1 : max_inflight),
+          alive_(std::make_shared<bool>(true))
+    {
+        if (!batch_) return;
+        ring_ = static_cast<uint8_t*>(kmws_host_alloc(ring_bytes, device));
+        if (ring_ && kmws_tx_batch_attach_ring(batch_, ring_, ring_bytes) == KMWS_OK) {
+            ring_bytes_ = ring_bytes;
+        } else {
+            kmws_host_free(ring_);
+            ring_ = nullptr;
+        }
+    }
+    ~TxLoop()
+    {
+        *alive_ = false;  // a posted task still queued on the loop becomes a no-op
+        if (batch_) {
+            (void)flush();  // every queued frame is written: close connections first
+            kmws_tx_batch_destroy(batch_);
+        }
+        kmws_host_free(ring_);
+    }
+    TxLoop(const TxLoop&) = delete;
+    TxLoop& operator=(const TxLoop&) = delete;
+
+    // The TxLoop of the calling (event-loop) thread, created on first use.
+    static TxLoop& forThisThread(Poster post, int device = 0)
+    {
+        thread_local TxLoop loop(std::move(post), device);
+        return loop;
+    }
+
+    bool valid() const { return batch_ != nullptr && ring_ != nullptr; }
+    void setPoster(Poster post) { post_ = std::move(post); }
+
+    // A connection's queue (kuma: per WebSocket::Impl, around ws_conn_->send).
+    Conn* open(Writer w)
+    {
+        conns_.emplace_back(new Conn(std::move(w)));
+        return conns_.back().get();
+    }
+    // Writes everything queued (every connection's frames), then forgets c.
+    int close(Conn* c)
+    {
+        const int r = flush();
+        for (size_t i = 0; i < conns_.size(); ++i)
+            if (conns_[i].get() == c) {
+                conns_.erase(conns_.begin() + (std::ptrdiff_t)i);
+                break;
+            }
+        return r;
+    }
+
+    // sendWsFrame(hdr, payload, plen) (WebSocketImpl.cpp:381-403): length =
+    // plen, header packed now; masked with hdr.maskey when hdr.mask is set and
+    // plen > 0 (kuma's client mode, :384-388).  Returns the header length
+    // (2..14) or a negative kmws_status.
+    int send(Conn* c, const kmws_frame_hdr& hdr, const uint8_t* payload, size_t plen)
+    {
+        const uint8_t* segs[1] = {payload};
+        const size_t lens[1] = {plen};
+        return sendChain(c, hdr, segs, lens, plen ? 1 : 0);
+    }
+
+    // sendWsFrame(hdr, KMBuffer) (:405-436): the chain's segments, the key
+    // phase continuing across them; more than 128 non-empty segments return
+    // KMWS_ERR_BUFFER_TOO_LONG and send nothing (as kuma, :427).
+    int sendChain(Conn* c, const kmws_frame_hdr& hdr, const uint8_t* const* segs, const size_t* lens, size_t nseg)
+    {
+        if (!valid() || !c) return KMWS_ERR_INVALID_STATE;
+        size_t plen = 0, nonempty = 0;
+        for (size_t i = 0; i < nseg; ++i) {
+            plen += lens[i];
+            nonempty += lens[i] != 0;
+        }
+        if (nonempty > 128) return KMWS_ERR_BUFFER_TOO_LONG;
+        if (plen > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+        Frame f;
+        f.conn = c;
+        f.plen = plen;
+        kmws_frame_hdr h = hdr;
+        h.length = (uint32_t)plen;
+        const bool masked = h.mask && plen > 0;
+        if (!masked && c->queued_ == 0) {  // nothing of this connection is waiting: sendWsFrame's own path
+            uint8_t hb[KMWS_MAX_HEADER_SIZE];
+            const int hl = kmws_encode_header(&h, hb);
+            std::vector<iovec> iov(1, iovec{hb, (size_t)hl});
+            for (size_t i = 0; i < nseg; ++i)
+                if (lens[i]) iov.push_back(iovec{const_cast<uint8_t*>(segs[i]), lens[i]});
+            c->last_ = c->write_(iov.data(), (int)iov.size());
+            return hl;
+        }
+        uint8_t* p = place(plen, &f);
+        if (!p) return KMWS_ERR_FAILED;
+        for (size_t i = 0, pos = 0; i < nseg; pos += lens[i], ++i)
+            if (lens[i]) std::memcpy(p + pos, segs[i], lens[i]);
+        f.payload = p;
+        if (masked) {
+            size_t one = plen;
+            f.hlen = kmws_tx_batch_add(batch_, &h, &p, &one, 1, f.hdr);
+            cur_.masked = true;
+        } else {
+            f.hlen = kmws_encode_header(&h, f.hdr);
+        }
+        if (f.hlen < 0) return f.hlen;
+        cur_.frames.push_back(std::move(f));
+        ++c->queued_;
+        arm();
+        return cur_.frames.back().hlen;
+    }
+
+    // Posts the iteration's task once (after a send).
+    void arm()
+    {
+        if (armed_ || !post_) return;
+        armed_ = true;
+        std::weak_ptr<bool> alive = alive_;
+        post_([this, alive] {
+            std::shared_ptr<bool> a = alive.lock();
+            if (a && *a) runIteration();
+        });
+    }
+
+    // The posted task: submit the iteration's masks, write every generation
+    // whose masks completed, keep at most max_inflight generations in flight;
+    // re-arms itself while any are.
+    void runIteration()
+    {
+        armed_ = false;
+        int r = submit();
+        if (r >= 0) r = complete(false);
+        while (r >= 0 && (int)inflight_.size() > max_inflight_) r = completeOldest();
+        last_ = r;
+        if (!inflight_.empty()) arm();
+    }
+
+    // Everything sent so far masked and written, synchronously.
+    int flush()
+    {
+        int r = submit();
+        if (r >= 0) r = complete(true);
+        return last_ = r;
+    }
+
+    int inflight() const { return (int)inflight_.size(); }
+    int pending() const { return (int)cur_.frames.size(); }
+    int lastResult() const { return last_; }  // frames written by the last run, or a kmws_status
+
+private:
+    struct Frame {
+        Conn* conn = nullptr;
+        uint8_t hdr[KMWS_MAX_HEADER_SIZE];
+        int hlen = 0;
+        uint8_t* payload = nullptr;
+        size_t plen = 0;
+        std::unique_ptr<uint8_t[]> own;  // a payload larger than the ring
+    };
+    struct Gen {
+        std::vector<Frame> frames;
+        bool masked = false;
+        int64_t ticket = 0;
+        size_t ring_used = 0;  // ring bytes (with alignment and wrap waste) freed when written
+    };
+
+    // Room for n payload bytes: 16-byte aligned in the ring, after the bytes
+    // in use (written generations free theirs in order); a full ring writes
+    // the oldest generation first; a payload larger than the ring gets a heap
+    // buffer (staged by the tx batch).
+    uint8_t* place(size_t n, Frame* f)
+    {
+        if (n == 0) return ring_;
+        if (n + 16 > ring_bytes_) {
+            f->own.reset(new (std::nothrow) uint8_t[n]);
+            return f->own.get();
+        }
+        for (;;) {
+            const size_t head = (tail_ + used_) % ring_bytes_;
+            const size_t pad = (16 - (head & 15)) & 15;
+            size_t waste = pad, at = head + pad;
+            if (at + n > ring_bytes_) {  // wrap: the end of the ring stays unused
+                waste = ring_bytes_ - head;
+                at = 0;
+            }
+            if (used_ + waste + n <= ring_bytes_) {
+                used_ += waste + n;
+                cur_.ring_used += waste + n;
+                return ring_ + at;
+            }
+            // full: free the oldest generation, or everything if only the current one holds the ring
+            const int r = inflight_.empty() ? flush() : completeOldest();
+            if (r < 0) return nullptr;
+        }
+    }
+
+    int submit()
+    {
+        if (cur_.frames.empty()) return 0;
+        if (cur_.masked) {
+            const int64_t t = kmws_tx_batch_submit(batch_);
+            if (t < 0) return (int)t;
+            cur_.ticket = t;
+        }
+        inflight_.push_back(std::move(cur_));
+        cur_ = Gen();
+        return 0;
+    }
+
+    // Writes finished generations in order (wait: all of them); returns the
+    // frames written or a negative status.
+    int complete(bool wait)
+    {
+        int n = 0;
+        while (!inflight_.empty()) {
+            Gen& g = inflight_.front();
+            if (g.ticket > 0) {
+                const int p = kmws_tx_batch_poll(batch_, g.ticket, wait ? 1 : 0);
+                if (p < 0) return p;
+                if (p == 0) break;
+            }
+            n += write(g);
+            used_ -= g.ring_used;
+            tail_ = (tail_ + g.ring_used) % ring_bytes_;
+            inflight_.pop_front();
+        }
+        if (inflight_.empty() && cur_.frames.empty() && cur_.ring_used == 0) tail_ = used_ = 0;
+        return n;
+    }
+    int completeOldest()
+    {
+        Gen& g = inflight_.front();
+        if (g.ticket > 0) {
+            const int p = kmws_tx_batch_poll(batch_, g.ticket, 1);
+            if (p < 0) return p;
+        }
+        const int n = write(g);
+        used_ -= g.ring_used;
+        tail_ = (tail_ + g.ring_used) % ring_bytes_;
+        inflight_.pop_front();
+        return n;
+    }
+
+    // Each connection's consecutive frames of the generation as one writev
+    // (kuma's send takes an iovec array, :432), at most 1024 entries at a time.
+    int write(Gen& g)
+    {
+        std::vector<iovec> iov;
+        Conn* c = nullptr;
+        auto out = [&] {
+            if (c && !iov.empty()) c->last_ = c->write_(iov.data(), (int)iov.size());
+            iov.clear();
+        };
+        for (Frame& f : g.frames) {
+            if (f.conn != c || iov.size() + 2 > 1024) {
+                out();
+                c = f.conn;
+            }
+            iov.push_back(iovec{f.hdr, (size_t)f.hlen});
+            if (f.plen) iov.push_back(iovec{f.payload, f.plen});
+            --f.conn->queued_;
+        }
+        out();
+        return (int)g.frames.size();
+    }
+
+    Poster post_;
+    kmws_tx_batch* batch_;
+    int max_inflight_;
+    std::shared_ptr<bool> alive_;
+    uint8_t* ring_ = nullptr;
+    size_t ring_bytes_ = 0;
+    size_t tail_ = 0, used_ = 0;  // ring bytes in use: [tail_, tail_ + used_) mod ring_bytes_
+    Gen cur_;
+    std::deque<Gen> inflight_;
+    std::vector<std::unique_ptr<Conn>> conns_;
+    bool armed_ = false;
+    int last_ = 0;
 };
 
 template <class FrameHeader, class Buffer, class WSError, class WSMode, class CbResult>

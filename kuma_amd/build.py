@@ -16,11 +16,18 @@ ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libkmws_gpu.so")
 ARCH = "gfx950"
-# Test-only variant (never loaded by kuma_amd.kmws): one tile of the header-pack
-# look-back never publishes and the spin bound is small, so the timeout path
-# (kStatusLookbackTimeout) runs in tests/test_gpu_pack.py.
-LOOKBACK_TEST_LIB = os.path.join(LIB_DIR, "libkmws_gpu_lbtest.so")
-LOOKBACK_TEST_DEFINES = ("KMWS_TEST_SKIP_PUBLISH_TILE=1", "KMWS_LOOKBACK_SPIN_LIMIT=4096")
+# Test-only variant (never loaded by kuma_amd.kmws; tests load it by path):
+#  - one tile of every look-back scan never publishes and the spin bound is
+#    small, so the timeout path (kStatusLookbackTimeout) runs in
+#    tests/test_gpu_pack.py;
+#  - a resident-worker job whose first key is 0xDEAD5Exx stalls its workgroup
+#    for xx * 10 ms, and the job timeout / drain bounds are 50 / 150 ms, so the
+#    withdraw and KMWS_ERR_TIMEOUT paths run in tests/test_gpu_decoder.py.
+TEST_LIB = os.path.join(LIB_DIR, "libkmws_gpu_testhooks.so")
+TEST_DEFINES = ("KMWS_TEST_SKIP_PUBLISH_TILE=1", "KMWS_LOOKBACK_SPIN_LIMIT=4096",
+                "KMWS_TEST_RESIDENT_STALL_KEY=0xDEAD5E00u", "KMWS_RESIDENT_TIMEOUT_MS=50",
+                "KMWS_RESIDENT_DRAIN_MS=150")
+RESIDENT_STALL_KEY = 0xDEAD5E00
 
 
 def sources():
@@ -72,10 +79,10 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
 
 def build_test_variants(force: bool = False) -> list:
     """Test-only libraries (tests load them by path; the product binding never does)."""
-    if force or not os.path.exists(LOOKBACK_TEST_LIB) or os.path.getmtime(LOOKBACK_TEST_LIB) < max(
+    if force or not os.path.exists(TEST_LIB) or os.path.getmtime(TEST_LIB) < max(
             os.path.getmtime(p) for p in deps()):
-        build(out=LOOKBACK_TEST_LIB, defines=LOOKBACK_TEST_DEFINES)
-    return [LOOKBACK_TEST_LIB]
+        build(out=TEST_LIB, defines=TEST_DEFINES)
+    return [TEST_LIB]
 
 
 if __name__ == "__main__":

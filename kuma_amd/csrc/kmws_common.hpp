@@ -97,20 +97,35 @@ inline uint64_t piece_count(uint64_t off, uint32_t len)
 kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,
                                  hipStream_t s);
 
-// Resident worker (kmws_resident.hip): synchronous host jobs of at most
-// kResMaxDescs payloads and kResMaxBytes bytes go to a workgroup that stays on
-// the GPU polling pinned memory, instead of a launch + wait per call.
+// Resident worker (kmws_resident.hip): host jobs of at most kResMaxDescs
+// payloads and kResMaxBytes bytes go to the calling thread's slot of a grid
+// that stays on the GPU polling pinned memory, instead of a launch per call.
 constexpr int kResMaxDescs = 128;
 // One workgroup moves a job over PCIe at ~3 GB/s: at 64 KiB it is as fast as a
 // launch of the multi-block pieces kernel (20 us each, tests/cpp/rx_flush_bench.cpp,
 // profiles/r04w_rx_flush_bench.jsonl), below it faster (10.7 vs 18.5 us at 16
 // KiB); above it the launch's several blocks move the bytes faster.
 constexpr uint64_t kResMaxBytes = 64u << 10;
-// Unmasks descs[0..n) over dev_base and descs2[0..n2) over dev_base2 (device
-// views of pinned host memory, offsets relative to them), synchronously.
-// KMWS_ERR_NOT_SUPPORTED: too large for one job, the calling thread switched
-// the worker off, or it is unusable -- the caller launches instead.  Any other
-// error: the job may or may not have run.
+struct ResidentJob {
+    int device = -1;
+    int slot = -1;
+    uint64_t seq = 0;
+};
+// Posts the unmask of descs[0..n) over dev_base and descs2[0..n2) over
+// dev_base2 (device views of pinned host memory, offsets relative to them) on
+// the calling thread's slot and returns at once.  KMWS_ERR_NOT_SUPPORTED
+// (nothing posted): too large for one job, no slot free, the thread switched
+// the worker off, its slot still runs a job, or the worker is unusable -- the
+// caller launches instead.
+kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
+                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job);
+// 1: done; 0: running; KMWS_ERR_NOT_SUPPORTED: withdrawn, never run (launch it).
+int resident_test(const ResidentJob& job);
+// KMWS_OK: done.  KMWS_ERR_NOT_SUPPORTED: withdrawn, never run (launch it).
+// KMWS_ERR_TIMEOUT: neither finished nor abandoned in time -- the device may
+// still write the payloads, so their memory must not be reused.
+kmws_status resident_wait(const ResidentJob& job);
+// post + wait.
 kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
                             const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2);
 

@@ -55,9 +55,11 @@ inline size_t grow(size_t need, size_t have)
 }
 
 // A batch of payloads unmasked in place by the GPU.  Payloads are appended to
-// a pinned host area (16-B aligned starts); launch() enqueues the pieces kernel
-// on the pinned area itself (zero-copy over PCIe) on the stage's own stream and
-// records its completion event; run() = launch() + wait.  An optional second
+// a pinned host area (16-B aligned starts); launch() posts them as one job on
+// the calling thread's slot of the resident worker when they fit one, else
+// enqueues the pieces kernel on the pinned area itself (zero-copy over PCIe)
+// on the stage's own stream and records its completion event; done() / wait()
+// follow whichever ran; run() = launch() + wait.  An optional second
 // batch of descriptors can target another pinned buffer (a caller's registered
 // receive or send ring).  The asynchronous rx / tx batches keep one stage per
 // generation in flight (kmws_decoder.cpp).
@@ -124,48 +126,53 @@ public:
     }
 
     // Unmask every staged descriptor (and `extra` over `extra_base`, a pinned
-    // buffer of extra_span bytes, if given), then wait for the GPU.  One launch
-    // per buffer (launch_unmask_pieces) reading descriptors and piece list from
-    // pinned memory: no plan kernels, no copies, no status read-back.
-    // Small jobs go to the device's resident worker (no launch, no event wait;
-    // kmws_resident.hip); larger ones are launched on the stage's stream.
-    // extra_dv: the device view of extra_base if the caller has it (a ring
-    // attached once); else it is looked up here (hipPointerGetAttributes).
+    // buffer of extra_span bytes, if given), then wait for the GPU: launch() +
+    // wait().  extra_dv: the device view of extra_base if the caller has it (a
+    // ring attached once); else it is looked up here (hipPointerGetAttributes).
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                     const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
     {
-        const size_t n2 = extra ? extra->size() : 0;
-        if (n2 && !extra_dv) extra_dv = static_cast<uint8_t*>(device_view(extra_base));
-        if (descs_.size() + n2 <= (size_t)kResMaxDescs && descs_.size() + n2 > 0) {
-            bool ok = true;
-            for (size_t i = 0; i < n2; ++i) ok &= (*extra)[i].off + (*extra)[i].len <= extra_span;
-            if (!ok) return KMWS_ERR_INVALID_PARAM;
-            const uint8_t* dv2 = n2 ? extra_dv : nullptr;
-            if (n2 && !dv2) return KMWS_ERR_INVALID_PARAM;
-            if (descs_.size() && !dv_h_) return KMWS_ERR_FAILED;
-            const kmws_status st = resident_unmask(device_, descs_.data(), dv_h_, descs_.size(),
-                                                   n2 ? extra->data() : nullptr, dv2, n2);
-            if (st != KMWS_ERR_NOT_SUPPORTED) return st;
-        }
         kmws_status st = launch(extra_base, extra_span, extra, extra_dv);
         if (st != KMWS_OK) return st;
         return wait();
     }
 
     // Has the last launch() finished?  (true when nothing was launched)
-    bool done() const
+    bool done()
     {
         if (!launched_) return true;
+        if (res_pending_) {
+            const int r = resident_test(res_);
+            if (r == 1) return true;
+            if (r == 0) return false;
+            res_pending_ = false;
+            if (r != KMWS_ERR_NOT_SUPPORTED || launch_saved() != KMWS_OK) return true;  // wait() reports it
+        }
         const hipError_t e = hipEventQuery(done_);
         if (e == hipErrorNotReady) return false;
         (void)hipGetLastError();
         return true;  // finished, or failed: wait() reports which
     }
-    // Spins on the event for up to kSpinWaitUs first (a loop thread waiting for
-    // a small job should not be parked and woken by the runtime), then parks.
+    // A launched job: spins on the event for a time that grows with its bytes
+    // (a loop thread waiting for a small job should not be parked and woken by
+    // the runtime; a large one should not burn a core), then parks.
     kmws_status wait()
     {
         if (!launched_) return KMWS_OK;
+        if (res_pending_) {
+            res_pending_ = false;
+            const kmws_status st = resident_wait(res_);
+            if (st == KMWS_ERR_TIMEOUT) abandon();
+            if (st != KMWS_ERR_NOT_SUPPORTED) {
+                launched_ = false;
+                return st;
+            }
+            const kmws_status ls = launch_saved();  // withdrawn, never run: launch it now
+            if (ls != KMWS_OK) {
+                launched_ = false;
+                return ls;
+            }
+        }
         launched_ = false;
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
@@ -175,15 +182,64 @@ public:
                 (void)hipGetLastError();
                 return KMWS_ERR_FAILED;
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinWaitUs)) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
         }
         return hipEventSynchronize(done_) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
     }
-    static constexpr int kSpinWaitUs = 2000;
 
-    // Enqueue the unmask of every staged descriptor (and `extra`) without waiting.
+    // Enqueue the unmask of every staged descriptor (and `extra`) without
+    // waiting: a job of at most kResMaxDescs payloads and kResMaxBytes bytes is
+    // posted on the calling thread's slot of the device's resident worker (no
+    // launch; kmws_resident.hip), anything else is launched on the stage's
+    // stream (launch_unmask_pieces: no plan kernels, no copies, no status
+    // read-back) with its completion event recorded.
     kmws_status launch(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                        const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
+    {
+        const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
+        if (n1 + n2 == 0) return KMWS_OK;
+        if (launched_) return KMWS_ERR_INVALID_STATE;
+        for (size_t i = 0; i < n2; ++i)
+            if ((*extra)[i].off + (*extra)[i].len > extra_span) return KMWS_ERR_INVALID_PARAM;
+        if (n2 && !extra_dv) extra_dv = static_cast<uint8_t*>(device_view(extra_base));
+        if (n2 && !extra_dv) return KMWS_ERR_INVALID_PARAM;  // must be pinned
+        if (n1 && !dv_h_) return KMWS_ERR_FAILED;
+        if (n1 + n2 <= (size_t)kResMaxDescs) {
+            const kmws_status st = resident_post(device_, descs_.data(), dv_h_, n1, n2 ? extra->data() : nullptr,
+                                                 extra_dv, n2, &res_);
+            if (st == KMWS_OK) {  // kept for a launch if the worker withdraws the job
+                saved_base_ = extra_base;
+                saved_span_ = extra_span;
+                saved_dv_ = extra_dv;
+                saved_extra_.assign(extra ? extra->begin() : saved_extra_.end(), extra ? extra->end() : saved_extra_.end());
+                res_pending_ = true;
+                launched_ = true;
+                return KMWS_OK;
+            }
+            if (st != KMWS_ERR_NOT_SUPPORTED) return st;
+        }
+        return launch_kernels(extra_base, extra_span, extra, extra_dv);
+    }
+
+private:
+    kmws_status launch_saved()
+    {
+        return launch_kernels(saved_base_, saved_span_, saved_extra_.empty() ? nullptr : &saved_extra_, saved_dv_);
+    }
+
+    // The device may still write the staging area (a resident job that timed
+    // out): it is left to the device -- never freed, never reused.
+    void abandon()
+    {
+        h_ = nullptr;
+        dv_h_ = nullptr;
+        cap_ = 0;
+        len_ = 0;
+        descs_.clear();
+    }
+
+    kmws_status launch_kernels(uint8_t* extra_base, uint64_t extra_span, const std::vector<kmws_desc>* extra,
+                               uint8_t* extra_dv)
     {
         const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
         if (n1 + n2 == 0) return KMWS_OK;
@@ -191,12 +247,16 @@ public:
         // the extra buffer's 16-B aligned base, descriptors rebased onto it
         uint8_t* eb = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(extra_base) & ~(uintptr_t)15);
         const uint64_t delta = (uint64_t)(extra_base - eb);
-        uint64_t p1 = 0, p2 = 0;
-        for (const kmws_desc& x : descs_) p1 += piece_count(x.off, x.len);
+        uint64_t p1 = 0, p2 = 0, bytes = 0;
+        for (const kmws_desc& x : descs_) {
+            p1 += piece_count(x.off, x.len);
+            bytes += x.len;
+        }
         for (size_t i = 0; i < n2; ++i) {
             const kmws_desc& x = (*extra)[i];
             if (x.off + x.len > extra_span) return KMWS_ERR_INVALID_PARAM;
             p2 += piece_count(x.off + delta, x.len);
+            bytes += x.len;
         }
         if (p1 + p2 > 0x7FFFFFFFull) return KMWS_ERR_INVALID_PARAM;
         kmws_status st = ensure_host(n1 + n2, p1 + p2);
@@ -227,11 +287,12 @@ public:
             if (st != KMWS_OK) return st;
         }
         if (hipEventRecord(done_, stream_) != hipSuccess) return KMWS_ERR_FAILED;
+        // ~16 GB/s over PCIe: 64 KiB ~ 4 us on top of a launch's ~50 us
+        spin_us_ = std::min<uint64_t>(2000, 50 + (bytes >> 14));
         launched_ = true;
         return KMWS_OK;
     }
 
-private:
     // Pinned descriptor and piece arrays (and their device views) for nd / np entries.
     kmws_status ensure_host(size_t nd, size_t np)
     {
@@ -265,6 +326,7 @@ private:
     }
     void release()
     {
+        if (launched_) (void)wait();  // nothing may outlive its pinned memory (a timed-out job's is abandoned)
         if (stream_) (void)hipStreamSynchronize(stream_);
         if (done_) (void)hipEventDestroy(done_);
         if (h_) (void)hipHostFree(h_);
@@ -278,6 +340,13 @@ private:
     hipStream_t stream_ = nullptr;
     hipEvent_t done_ = nullptr;
     bool launched_ = false;
+    bool res_pending_ = false;  // launched_ on the resident worker: res_ says which job
+    ResidentJob res_;
+    uint8_t* saved_base_ = nullptr;  // extra of a resident job, for launch_saved()
+    uint64_t saved_span_ = 0;
+    uint8_t* saved_dv_ = nullptr;
+    std::vector<kmws_desc> saved_extra_;
+    uint64_t spin_us_ = 50;
     uint8_t* h_ = nullptr;
     uint8_t* dv_h_ = nullptr;
     size_t cap_ = 0, len_ = 0;

@@ -79,27 +79,17 @@ struct V2 {
 };
 __device__ __forceinline__ V2 operator+(V2 x, V2 y) { return V2{x.a + y.a, x.b + y.b}; }
 
-#ifndef KMWS_UNIT_LANE_WORDS
-#define KMWS_UNIT_LANE_WORDS 4
-#endif
 // Output words per wave unit: 4 per lane (4 KiB).  2, 3, 5, 6 and 8 words per
 // lane measured the same or slower on cfg3/cfg4/64 KiB frames (round 1); again
 // this round, 5 and 6 words per lane (one unit per 4 KiB fragment instead of
 // two): cfg4 encode 0.57 / 0.60 against 0.73 (profiles/r03aq_unit_words_ab.txt).
-constexpr int kUnitWords = 64 * KMWS_UNIT_LANE_WORDS;
-#ifndef KMWS_COPY_SPLIT_DEFAULT
-#define KMWS_COPY_SPLIT_DEFAULT 8  // re-measured on plain allocations this round: 2 / 4 / 16 / XCD runs all slower
-#endif                              // on cfg4 and cfg3 (profiles/r03bi_copy_split_ab.txt)
-constexpr uint32_t kCopySplit = KMWS_COPY_SPLIT_DEFAULT;
-#ifndef KMWS_CHUNK_SPLIT
-#define KMWS_CHUNK_SPLIT 4  // the chunk grid's parts (r04r: 4 > 8 > 16 on cfg4)
-#endif
-constexpr uint32_t kChunkSplit = KMWS_CHUNK_SPLIT;
+constexpr int kUnitWords = 64 * 4;
+// The unit copy grid's parts: 2 / 4 / 16 / XCD runs all slower on cfg4 and
+// cfg3 (profiles/r03bi_copy_split_ab.txt).
+constexpr uint32_t kCopySplit = 8;
+constexpr uint32_t kChunkSplit = 4;  // the chunk grid's parts (r04r: 4 > 8 > 16 on cfg4)
 constexpr uint64_t kUnitAlign = 64;  // unit bases: 1 KiB aligned in the output
-#ifndef KMWS_LINE_BYTES
-#define KMWS_LINE_BYTES 64
-#endif
-constexpr uint64_t kLineBytes = KMWS_LINE_BYTES;  // ownership granule: 64 B keeps a frame edge at 1 + 4 words
+constexpr uint64_t kLineBytes = 64;  // ownership granule: 64 B keeps a frame edge at 1 + 4 words
 constexpr uint64_t kLineWords = kLineBytes / 16;
 constexpr int kEdgeWords = 1 + (int)kLineWords;   // owned non-interior words per frame (at most)
 
@@ -518,13 +508,6 @@ struct FrameUnits {
 // stored by the copy waves, which clip at the total.  Also the capacity check
 // (status set if the output exceeds cap; nothing is written then).
 //
-#ifdef KMWS_AB_TRACE_PRO  // tuning build only: per-block timestamps (s_memrealtime, 100 MHz) of the prologue
-__device__ uint64_t g_trace_pro[(1u << 16) * 8];
-#define KMWS_TRACE_PRO(ev) \
-    do { if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) g_trace_pro[blockIdx.x * 8 + (ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define KMWS_TRACE_PRO(ev) do { } while (0)
-#endif
 // The prologue's per-row part (prologue_kernel; round 4's rejected fused row
 // kernel shared it, profiles/r04i_pack_rows_ab.txt):
 // row `row`'s frame offsets (written to start[]), its frames' unit geometry
@@ -556,7 +539,6 @@ __device__ __forceinline__ bool row_prologue(uint32_t rid, const uint8_t* __rest
     uint8_t* s_ne = L.ne;
     V2* s_w = L.w;
     const uint32_t t = threadIdx.x;
-    KMWS_TRACE_PRO(0);
     const uint64_t F0 = (uint64_t)rid * kBlock;
     const uint32_t nf = n - F0 < (uint64_t)kBlock ? (uint32_t)(n - F0) : (uint32_t)kBlock;
     const uint32_t f = (uint32_t)(F0 + (t < nf ? t : nf - 1));
@@ -572,7 +554,6 @@ __device__ __forceinline__ bool row_prologue(uint32_t rid, const uint8_t* __rest
     const uint64_t rsz = (uint64_t)(HEADERS ? hdr_len(x[0].len, (fl[0] >> 8) & 1u) : 0u) + x[0].len;
     const V2 off = pre + block_excl_scan(t < nf ? V2{rsz, unit_bound(rsz)} : V2{0, 0}, s_w, row);
     const uint64_t r0 = off.a, uf = off.b, S0 = pre.b, uend = pre.b + row.b;
-    KMWS_TRACE_PRO(1);
     if (t < nf) start[f] = r0;
     ri.F0 = F0;
     ri.S0 = S0;
@@ -631,7 +612,6 @@ __device__ __forceinline__ bool row_prologue(uint32_t rid, const uint8_t* __rest
             k = k < wlo ? wlo : (k > whi ? whi : k);
             S[j] = *reinterpret_cast<const u32x4*>(src + (nlive ? 16 * (uint64_t)k : 0));
         }
-        KMWS_TRACE_PRO(2);
         u32x4* my = s_edge + t * kEdgeWords;
         uint32_t third = 0;
         if (head_f && nedge) {
@@ -722,7 +702,6 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
     const uint32_t* s_ub = L.ub;
     const u32x4* s_edge = L.edge;
     const uint8_t* s_ne = L.ne;
-    KMWS_TRACE_PRO(3);
     // edge words of the block's frames: one contiguous run, whole 128-byte lines
     // (the run starts on one: 256 frames x 80 B), skipping lines without a live
     // word (a line written in part costs more than writing it whole)
@@ -737,7 +716,6 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         if (j0 + 2 < nf && j0 + 2 <= j1) live |= s_ne[j0 + 2] != 0;
         if (live) eout[i] = s_edge[i];  // dead words of a live line: any value (never read)
     }
-    KMWS_TRACE_PRO(4);
     // unit records, slot-parallel
     const uint32_t ns = s_ub[nf];
     for (uint32_t sl = t; sl < ns; sl += kBlock) {
@@ -758,7 +736,6 @@ __global__ void __launch_bounds__(kBlock) prologue_kernel(const uint8_t* __restr
         }
         rec[S0 + sl] = r;
     }
-    KMWS_TRACE_PRO(5);
 }
 
 __device__ __forceinline__ u32x4 shfl16(const u32x4& v, int lane)
@@ -797,9 +774,6 @@ __device__ __forceinline__ UnitInfo decode_unit(const UnitRec& r, bool live, con
 // Source loads of the copy waves: non-temporal (streaming) by default.  A
 // shifted source run of 1 KiB per wave instruction starts mid-line, so two
 // instructions (or two waves) share its edge lines.
-#ifndef KMWS_COPY_NT_LOAD
-#define KMWS_COPY_NT_LOAD 1
-#endif
 constexpr int kUnitW = kUnitWords / 64;  // words per lane
 struct UnitRegs {
     u32x4 lo[kUnitW];  // aligned source word of each of the lane's output words
@@ -827,11 +801,7 @@ __device__ __forceinline__ void unit_issue(const UnitInfo& x, int lane, const ui
     for (int i = 0; i < kUnitW; ++i) {
         const uint32_t k = lane + 64 * i;
         const uint32_t kk = k < lo_k ? lo_k : (k < hi_k ? k : hi_k);
-#if KMWS_COPY_NT_LOAD
         R.lo[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + 16u * kk));
-#else
-        R.lo[i] = *reinterpret_cast<const u32x4*>(s0 + 16u * kk);
-#endif
     }
     // word last + 1 holds payload bytes only when the source is shifted (delta != 0)
     uint32_t xk = x.fast && x.delta ? x.last + 1 : hi_k;
@@ -977,10 +947,8 @@ __device__ __forceinline__ u32x4 shfl16_down1(const u32x4& v)
 // more fetched on cfg4) and wrote 80 B of edge words and two
 // 32 B unit records per 4 KiB frame; here their values join the chunk's four
 // full-width stores through LDS.
-#ifndef KMWS_CHUNK_LANE_WORDS
-#define KMWS_CHUNK_LANE_WORDS 4
-#endif
-constexpr uint32_t kChunkW = KMWS_CHUNK_LANE_WORDS;  // words per lane (4 or 8)
+// 4 words per lane (8 measured slower: 103 VGPRs, 4 waves per SIMD, 0.715 on cfg4)
+constexpr uint32_t kChunkW = 4;
 constexpr uint32_t kChunkWords = 64 * kChunkW;
 constexpr uint64_t kChunkBytes = 16ull * kChunkWords;
 constexpr uint32_t kSlowShift = 9;  // boundary-list entry: word | table frame << kSlowShift
@@ -1082,18 +1050,15 @@ __device__ __forceinline__ void store_word_bytes(uint8_t* __restrict__ dst, uint
     }
 }
 
-template <bool NT>
+// The chunk copy's source loads: non-temporal (streaming) for every batch.
 __device__ __forceinline__ u32x4 copy_src_load(const uint8_t* p)
 {
-    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return *reinterpret_cast<const u32x4*>(p);
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
 // One wave per 4 KiB output chunk (4 words per lane, 1 KiB per instruction).
 // A chunk meeting more than kChunkFrames frames is listed for chunk_dense_kernel.
-// NT: non-temporal source loads (batches of large frames); ordinary loads keep
-// the source lines two neighbouring chunks share in the L2 (small frames).
-template <bool HEADERS, bool NT>
+template <bool HEADERS>
 __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                             const kmws_desc* __restrict__ d,
                                                             const uint16_t* __restrict__ flags, uint32_t n,
@@ -1229,9 +1194,6 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
             wave_lds_sync();  // the scratch slots are reused
         }
     };
-#ifdef KMWS_AB_SKIP_BOUNDARY  // tuning build only: boundary words left uncomposed (wrong output; times pass 3)
-    nslow = 0;
-#endif
     if (nslow) batch_issue(0);
     // Pass 2: interior words' source words, one aligned word each (all four
     // rounds issued before anything waits).
@@ -1244,12 +1206,12 @@ __global__ void __launch_bounds__(kBlock) chunk_copy_kernel(const uint8_t* __res
         const ChunkFrame& e = tab[(uint32_t)(jbits >> (6 * i)) & 63u];
         const bool inner = a < trel && a >= e.p0 && a + 16 <= e.r1;
         const uint64_t sa = e.sbase + (int64_t)a;
-        L0[i] = copy_src_load<NT>(inner ? reinterpret_cast<const uint8_t*>(sa & ~15ull) : src);
+        L0[i] = copy_src_load(inner ? reinterpret_cast<const uint8_t*>(sa & ~15ull) : src);
         if (exr == (uint32_t)i) xa = (sa + 15) & ~15ull;  // the aligned word holding the word's last source byte
         dl |= (uint32_t)(sa & 15u) << (4 * i);
         rk[i] = e.rk;
     }
-    X = copy_src_load<NT>(reinterpret_cast<const uint8_t*>(xa));
+    X = copy_src_load(reinterpret_cast<const uint8_t*>(xa));
     // Pass 3: the boundary words
     if (nslow) batch_put(0);
     for (uint32_t g0 = 16; g0 < nslow; g0 += 16) {  // wave-uniform
@@ -1400,6 +1362,17 @@ constexpr uint64_t kStAgg = 1ull, kStInc = 2ull;
 #define KMWS_LOOKBACK_SPIN_LIMIT (1u << 24)
 #endif
 constexpr uint32_t kLookSpinLimit = KMWS_LOOKBACK_SPIN_LIMIT;
+// Does this tile publish its state?  Always, except in the test build, where
+// one tile never does (a successor must time out).
+__device__ __forceinline__ bool tile_publishes(uint32_t tile)
+{
+#ifdef KMWS_TEST_SKIP_PUBLISH_TILE
+    return tile != (uint32_t)(KMWS_TEST_SKIP_PUBLISH_TILE);
+#else
+    (void)tile;
+    return true;
+#endif
+}
 
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
 {
@@ -1417,15 +1390,6 @@ __device__ __forceinline__ void lds_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
-
-#ifdef KMWS_AB_TRACE  // tuning build only: per-tile timestamps (s_memrealtime, 100 MHz) of the one-pass kernel
-constexpr int kTraceEv = 6;
-__device__ uint64_t g_trace[(1u << 16) * kTraceEv];
-#define KMWS_TRACE(tile, ev) \
-    do { if (threadIdx.x == 0 && (tile) < (1u << 16)) g_trace[(tile) * kTraceEv + (ev)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define KMWS_TRACE(tile, ev) do { } while (0)
-#endif
 
 // One wave: the exclusive prefix of tile `tile` (> 0).  Lane 0 first polls the
 // nearest predecessor; then lane l looks at the tile at distance l below
@@ -1479,7 +1443,6 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t tile = blockIdx.x;
     const uint64_t F = (uint64_t)tile * kScanTile;
-    KMWS_TRACE(tile, 0);
     // frames F + i * 256 + t: every load and store coalesced, all loads issued at once
     // (only {len, key}, the descriptor's second 8 bytes, and the flags)
     uint64_t lk[kScanItems];
@@ -1505,17 +1468,8 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
     uint64_t agg = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) agg += s_a[w];
-#ifdef KMWS_AB_NO_LOOKBACK  // tuning build only (tools/ab_pack_headers.py): the kernel without its dependency
-    const bool first = true;
-#else
     const bool first = tile == 0;
-#endif
-    KMWS_TRACE(tile, 1);
-#ifdef KMWS_TEST_SKIP_PUBLISH_TILE  // test build only: this tile never publishes (a successor must time out)
-    const bool publish = tile != (uint32_t)(KMWS_TEST_SKIP_PUBLISH_TILE);
-#else
-    constexpr bool publish = true;
-#endif
+    const bool publish = tile_publishes(tile);
     if (t == 0 && publish) st_agent(st + tile, first ? agg << 2 | kStInc : agg << 2 | kStAgg);
     // then the header slots (they need no offset; stores issued ahead of the
     // publish would delay it: the vector memory queue is in order) and the sizes
@@ -1548,14 +1502,12 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
         if (w < (int)wave) before += s_w[w];
     uint64_t pre = 0;
     if (!first) {
-        KMWS_TRACE(tile, 2);
         if (wave == 0) {
             const uint64_t p = look_back(st, tile, head);
             if (lane == 0) s_pre = p;
         }
         lds_barrier();
         pre = s_pre;
-        KMWS_TRACE(tile, 4);
         if (t == 0 && publish) st_agent(st + tile, (pre + agg) << 2 | kStInc);
     }
     if (t == 0 && F + kScanTile >= n) out[n] = pre + agg;  // the last tile: the total
@@ -1572,7 +1524,6 @@ __global__ void __launch_bounds__(kBlock, 8) pack_headers_chain_kernel(const kmw
         const uint64_t f = F + (uint64_t)i * kBlock + t;
         if (f < n) out[f] = s_sz[i * kBlock + t];
     }
-    KMWS_TRACE(tile, 5);
 }
 
 __global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict__ p, uint64_t words)
@@ -1581,7 +1532,7 @@ __global__ void __launch_bounds__(kBlock) zero_words_kernel(uint64_t* __restrict
         p[i] = 0;
 }
 
-// The chunk form's front in ONE pass (KMWS_CHUNK_ONE_PASS, the default): a 2048-frame
+// The chunk form's front in ONE pass: a 2048-frame
 // tile per block, the scan by decoupled look-back (the header-only pack's
 // machinery above), then the tile's region offsets and its chunks' first
 // frames -- in place of reduce_kernel + scan_tiles_kernel + chunk_map_kernel,
@@ -1625,7 +1576,8 @@ __global__ void __launch_bounds__(kBlock) chunk_scan_kernel(const kmws_desc* __r
     uint64_t agg = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) agg += s_a[w];
-    if (t == 0) st_agent(st + tile, tile == 0 ? agg << 2 | kStInc : agg << 2 | kStAgg);
+    const bool publish = tile_publishes(tile);
+    if (t == 0 && publish) st_agent(st + tile, tile == 0 ? agg << 2 | kStInc : agg << 2 | kStAgg);
     uint64_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) sum += s_sz[kScanItems * t + k];
@@ -1644,7 +1596,7 @@ __global__ void __launch_bounds__(kBlock) chunk_scan_kernel(const kmws_desc* __r
         }
         lds_barrier();
         pre = s_pre;
-        if (t == 0) st_agent(st + tile, (pre + agg) << 2 | kStInc);
+        if (t == 0 && publish) st_agent(st + tile, (pre + agg) << 2 | kStInc);
     }
     uint64_t run = pre + before + inc - sum;
 #pragma unroll
@@ -1771,42 +1723,20 @@ __global__ void __launch_bounds__(kBlock) walk_headers_kernel(const uint8_t* __r
 }
 
 // ------------------------------ host launchers ------------------------------
-// The copy form, by the mean region bound cap / n: below KMWS_PACK_CHUNK_BELOW
+// The copy form, by the mean region bound cap / n: below kChunkFormBelow
 // bytes the chunk form (chunk_map + chunk_copy), from it the unit form
 // (prologue: edge words, unit records; copy_kernel).  Measured on one box
 // (profiles/r04p_chunk_ab.txt): cfg4 (4 KiB frames) 0.748 / 0.772 chunk against
 // 0.722 / 0.741 units, 8 M frames of 1-300 B 0.38 / 0.48 against 0.055 /
 // 0.058, cfg3 (Zipf, 37 KiB mean, 97 % of the bytes in frames >= 16 KiB)
-// 0.733 / 0.776 against 0.775 / 0.797 (encode / gather).  Tuning builds:
-// KMWS_PACK_UNITS=1 forces the unit form, KMWS_PACK_UNITS=2 the chunk form.
-#ifndef KMWS_PACK_UNITS
-#define KMWS_PACK_UNITS 0
-#endif
-#ifndef KMWS_PACK_CHUNK_BELOW
-#define KMWS_PACK_CHUNK_BELOW 16384
-#endif
-static bool use_chunks(uint32_t n, uint64_t cap)
-{
-    if (KMWS_PACK_UNITS == 1) return false;
-    if (KMWS_PACK_UNITS == 2) return true;
-    return n && cap / n < (uint64_t)KMWS_PACK_CHUNK_BELOW;
-}
-// Chunk copy tuning by the mean region bound cap / n (tuning builds override):
-// non-temporal source loads from KMWS_CHUNK_NT_FROM bytes (measured: faster
-// for every batch, cfg4 0.77 / 0.79 against 0.76 / 0.76 encode / gather with
-// ordinary loads; profiles/r04o_chunk_ab.txt), and from KMWS_CHUNK_PAD_FROM
-// bytes KMWS_CHUNK_PAD_BYTES of dynamic LDS per block (19 KiB static + 13 KiB:
-// 5 blocks per CU -- the unit form's large-frame setting, 0.61 against 0.75 on
-// cfg3 here, so never by default).
-#ifndef KMWS_CHUNK_NT_FROM
-#define KMWS_CHUNK_NT_FROM 0
-#endif
-#ifndef KMWS_CHUNK_PAD_FROM
-#define KMWS_CHUNK_PAD_FROM 0xFFFFFFFFFFFFFFFFull
-#endif
-#ifndef KMWS_CHUNK_PAD_BYTES
-#define KMWS_CHUNK_PAD_BYTES 13312
-#endif
+// 0.733 / 0.776 against 0.775 / 0.797 (encode / gather).
+constexpr uint64_t kChunkFormBelow = 16384;
+static bool use_chunks(uint32_t n, uint64_t cap) { return n && cap / n < kChunkFormBelow; }
+// The chunk copy loads its source non-temporally for every batch (cfg4 0.77 /
+// 0.79 against 0.76 / 0.76 encode / gather with ordinary loads,
+// profiles/r04o_chunk_ab.txt) and runs without an LDS cap on its occupancy (5
+// blocks per CU, the unit form's large-frame setting, ran 0.61 against 0.75 on
+// cfg3).
 struct CopyWs {
     WsHead* head;
     V2* tiles;  // ntiles + 1: tile prefixes, then the totals
@@ -1881,13 +1811,11 @@ template <bool HEADERS>
 static kmws_status launch_copy_tail(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                     const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c, hipStream_t s);
 
-// The chunk form's front: one look-back pass (chunk_scan_kernel; 1) or reduce +
-// scan + chunk_map (0).  Same box (profiles/r04aq_chunk_one_pass_ab.txt): cfg4
+// The chunk form's front: one look-back pass (chunk_scan_kernel) in place of
+// reduce + scan + chunk_map (which the fused unpack-gather keeps: its scan
+// parses the headers).  Same box (profiles/r04aq_chunk_one_pass_ab.txt): cfg4
 // 0.752-0.767 / 0.774-0.779 against 0.749-0.766 / 0.772-0.777, 1-300 B frames
 // 0.35-0.40 / 0.45-0.49 against 0.34-0.39 / 0.44-0.48 (encode / gather).
-#ifndef KMWS_CHUNK_ONE_PASS
-#define KMWS_CHUNK_ONE_PASS 1
-#endif
 template <bool HEADERS>
 static kmws_status launch_chunks_one_pass(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
                                           const kmws_desc* d, const uint16_t* flags, uint32_t n, CopyWs& c,
@@ -1900,9 +1828,7 @@ static kmws_status launch_copy(const uint8_t* src, uint8_t* dst, uint64_t cap, u
         if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
         return launch_zero(start, sizeof(uint64_t), s);
     }
-#if KMWS_CHUNK_ONE_PASS
     if (use_chunks(n, cap)) return launch_chunks_one_pass<HEADERS>(src, dst, cap, start, d, flags, n, c, s);
-#endif
     const kmws_status st = HEADERS ? launch_reduce(WireSize{d, flags}, n, start, c, s)
                                    : launch_reduce(PayloadSize{d}, n, start, c, s);
     if (st != KMWS_OK) return st;
@@ -1924,7 +1850,7 @@ static kmws_status launch_chunks(const uint8_t* src, uint8_t* dst, uint64_t cap,
     return launch_chunk_copy<HEADERS>(src, dst, cap, start, d, flags, n, c, nt, s);
 }
 
-// The chunk form's front in one pass (KMWS_CHUNK_ONE_PASS):
+// The chunk form's front in one pass:
 // zero the head, the totals and the tile states, then chunk_scan_kernel.
 template <bool HEADERS>
 static kmws_status launch_chunks_one_pass(const uint8_t* src, uint8_t* dst, uint64_t cap, uint64_t* start,
@@ -1951,18 +1877,11 @@ static kmws_status launch_chunk_copy(const uint8_t* src, uint8_t* dst, uint64_t 
     const uint64_t chunks = chunk_count(cap);  // upper bound; waves past the total exit at once
     constexpr uint64_t kWaves = kBlock / 64;
     constexpr uint64_t kMaxChunksPerLaunch = ((1ull << 32) / kBlock / 2) * kWaves;
-    const uint64_t mean = cap / n;  // bounds the mean region size from above
-    const bool nt_loads = mean >= (uint64_t)KMWS_CHUNK_NT_FROM;
-    const unsigned lds_pad = mean >= (uint64_t)KMWS_CHUNK_PAD_FROM ? (unsigned)KMWS_CHUNK_PAD_BYTES : 0u;
     for (uint64_t c0 = 0; c0 < chunks; c0 += kMaxChunksPerLaunch) {
         const uint64_t nc = chunks - c0 < kMaxChunksPerLaunch ? chunks - c0 : kMaxChunksPerLaunch;
         const dim3 grid((uint32_t)((nc + kWaves - 1) / kWaves));
-        if (nt_loads)
-            hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, true>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags, n,
-                               start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
-        else
-            hipLaunchKernelGGL((chunk_copy_kernel<HEADERS, false>), grid, dim3(kBlock), lds_pad, s, src, dst, d, flags,
-                               n, start, c.cmap, c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
+        hipLaunchKernelGGL(chunk_copy_kernel<HEADERS>, grid, dim3(kBlock), 0, s, src, dst, d, flags, n, start, c.cmap,
+                           c.tiles + nt, c.head, c.dense, c0, kChunkSplit);
     }
     const uint32_t dense_blocks = (uint32_t)(chunks / kWaves < 512 ? chunks / kWaves + 1 : 512);
     hipLaunchKernelGGL(chunk_dense_kernel<HEADERS>, dim3(dense_blocks), dim3(kBlock), 0, s, src, dst, d, flags, n, start,
@@ -2055,18 +1974,6 @@ kmws_status kmws_unpack_gather(const uint8_t* wire, uint64_t wire_len, const uin
 }
 
 // head, then one 64-bit state per 2048-frame tile (pack_headers_chain_kernel)
-#ifdef KMWS_AB_TRACE_PRO
-int kmws_ab_trace_pro_read(uint64_t* host, size_t n_words)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_pro), n_words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
-#ifdef KMWS_AB_TRACE
-int kmws_ab_trace_read(uint64_t* host, size_t n_words)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), n_words * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 size_t kmws_pack_headers_workspace_size(uint32_t n) { return r16(sizeof(WsHead)) + n_tiles(n) * sizeof(uint64_t); }
 
 kmws_status kmws_pack_headers(const kmws_desc* descs, const uint16_t* flags, uint32_t n, uint8_t* hdr,

@@ -1,29 +1,35 @@
 // Resident unmask worker: the synchronous host entries without a kernel launch
-// per call.
+// per call, concurrent across the process's event-loop threads.
 //
 // kuma calls WSHandler::handleData once per <= 64 KiB socket read
 // (TcpConnection.cpp:229-233 -> WebSocketImpl.cpp:225-246) and
 // WSHandler::handleDataMask once per send (WebSocketImpl.cpp:388, :414), and
-// expects the payload unmasked when the call returns.  A stream launch plus an
-// event wait costs 13-15 us per call -- about what kuma's byte loop
-// (WSHandler.cpp:303-310) spends on a whole 64 KiB read -- so the synchronous
-// drop-in lost to the reference.  Here one workgroup of 1024
-// lanes stays resident on the GPU per device -- shared by the process's host
-// threads, one job at a time under a spin lock (a worker per thread measured
-// worse: two workers' streams share a hardware queue, so one thread's job
-// waited for the other's worker to leave, up to its lease) -- and polls a
-// mailbox in pinned host memory: the host writes a job (up to kResMaxDescs
-// payloads, each a device-visible address, a length and a key) and bumps the
-// job number; the worker sees it over PCIe, unmasks every payload in place
+// expects the payload unmasked when the call returns -- on every loop thread
+// (10 in kuma's test client, test/client/main.cpp:20; 5 in its server,
+// test/server/main.cpp:22).  A stream launch plus an event wait costs 13-15 us
+// per call, about what kuma's byte loop (WSHandler.cpp:303-310) spends on a
+// whole 64 KiB read.  Here ONE grid of kResSlots workgroups (1024 lanes each)
+// stays resident per device, on one greatest-priority stream: workgroup b
+// serves mailbox slot b, and a host thread claims a slot once (lock-free) and
+// keeps it until it exits.  Each slot is polled from pinned host memory by its
+// own workgroup: the thread writes a job (up to kResMaxDescs payloads, each a
+// device-visible address, a length and a key) and bumps the slot's job
+// number; the workgroup sees it over PCIe, unmasks every payload in place
 // there (zero-copy, 4 x 16-byte words per lane in flight: 64 KiB per round),
 // makes its stores visible system-wide and writes the job number back; the
-// host spins on that word.  No launch, no completion signal, no interrupt.
+// thread spins on that word.  No launch, no completion signal, no interrupt,
+// no lock: threads on different slots run their jobs at the same time.  A
+// thread that finds no free slot launches on its own stream instead; it never
+// waits for another thread.  (One grid, not a worker per thread: two workers'
+// greatest-priority streams shared a hardware queue, so one thread's job
+// waited for the other's worker to leave -- round 4, r04x.)
 //
-// The worker exits by itself after kResIdleUs (200 us) without a job, after a
-// lease of kResLeaseUs (1 ms) however busy it is, and on quit:
-// every wave reaches the exit, the grid drains, and a host thread that stops
-// feeding never leaves a kernel behind.  The next job relaunches it.  It runs
-// on a non-blocking stream of its own at the greatest priority, so work on
+// The grid exits by itself after kResIdleUs (200 us) without a job in any
+// slot, after a lease of kResLeaseUs (1 ms) however busy it is, and a
+// workgroup leaves on its slot's quit bit (process exit; a job past its
+// timeout): every wave reaches the exit, the grid drains, and a host thread
+// that stops feeding never leaves a kernel behind.  The next job relaunches
+// it.  The stream is non-blocking and of the greatest priority, so work on
 // other streams -- the legacy default stream included -- does not queue behind
 // it, and the lease bounds the wait of any kernel that still shares its
 // hardware queue (tests/test_gpu_decoder.py).
@@ -43,6 +49,11 @@ namespace kmws {
 
 constexpr int kResBlock = 1024;  // 16 waves: 4 words each = 64 KiB of loads in flight
 constexpr int kResWords = 4;
+// Slots per device: one per loop thread that uses the synchronous entries
+// (kuma's test client runs 10 loop threads, its server 5).  Unclaimed slots'
+// workgroups poll one word every few microseconds; a claimed slot's workgroup
+// polls its job word and 31 descriptor slots (512 B) back to back.
+constexpr int kResSlots = 16;
 // Idle exit: short.  The runtime maps streams onto a few hardware queues
 // (GPU_MAX_HW_QUEUES, 4 on the box), so a kernel launched on a stream that
 // shares the worker's queue waits until the worker leaves; and
@@ -52,20 +63,29 @@ constexpr int kResWords = 4;
 // from 2.0 to 0.57 GiB/s with a 5 ms idle).  A loop thread under load feeds far
 // more often than this; a worker that idled out costs one launch at the next
 // job, the price of every call without it.
-#ifndef KMWS_RESIDENT_IDLE_US
-#define KMWS_RESIDENT_IDLE_US 200
-#endif
-constexpr uint32_t kResIdleUs = KMWS_RESIDENT_IDLE_US;
+constexpr uint32_t kResIdleUs = 200;
 // Lease: an incarnation also leaves after kResLeaseUs of life however busy it
 // is, before it takes the next job (the host relaunches it for that job).  A
 // thread that feeds back to back would otherwise keep the worker resident for
 // good, and a kernel on another stream that shares its hardware queue would
 // wait for as long (measured: up to 6.9 s behind a feeder thread).  The
 // relaunch it costs (~10-15 us) is spread over the ~100 jobs of one lease.
-#ifndef KMWS_RESIDENT_LEASE_US
-#define KMWS_RESIDENT_LEASE_US 1000
+constexpr uint32_t kResLeaseUs = 1000;
+// A job not done after kResTimeoutMs is withdrawn: the slot's quit bit asks
+// its workgroup to leave, and the thread waits up to kResDrainMs more for it.
+// Only when the workgroup has left (or finished the job) does the call return
+// without KMWS_ERR_TIMEOUT -- nothing writes the payloads after that.  The
+// test build shortens both (kuma_amd/build.py).
+#ifndef KMWS_RESIDENT_TIMEOUT_MS
+#define KMWS_RESIDENT_TIMEOUT_MS 2000
 #endif
-constexpr uint32_t kResLeaseUs = KMWS_RESIDENT_LEASE_US;
+#ifndef KMWS_RESIDENT_DRAIN_MS
+#define KMWS_RESIDENT_DRAIN_MS 2000
+#endif
+// A job whose workgroup left while the rest of the grid still runs (it is
+// closing, or another workgroup is stuck in a job) is withdrawn after this long
+// and launched by the caller.
+constexpr uint32_t kResOrphanUs = 200;
 
 static inline void cpu_relax()
 {
@@ -81,24 +101,22 @@ struct ResDesc {  // one payload: device-visible address, bytes, LE key of its f
 };
 static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 
-// Pinned host memory, polled by the worker.  Host-written and device-written
-// words sit in different 128-byte lines.  The polled word carries the job
-// number (bits 0-39), the payload count (40-47) and the quit bit (63); the
-// first kPollDescs descriptor slots follow it and are read with it at every
-// poll, so a job of up to kPollDescs payloads costs one PCIe round trip to
-// notice and none more to read its descriptors.  The host rewrites every one
-// of those slots for every job (unused ones with length 0), each half of a
-// slot tagged with the job's low bits (address bits 48-63, length bits
-// 21-31): a slot read before the host's write landed carries the previous
+// The polled word of a slot: job number (bits 0-39), payload count (40-47),
+// claimed (62: a thread holds the slot, so its workgroup polls the
+// descriptors too) and quit (63).  The first kPollDescs descriptor slots
+// follow it and are read with it at every poll, so a job of up to kPollDescs
+// payloads costs one PCIe round trip to notice and none more to read its
+// descriptors.  The host rewrites every one of those slots for every job
+// (unused ones with length 0), each as two 8-byte stores tagged with the job's
+// low bits (address bits 48-63; length bits 21-31 in the half that also holds
+// the key): a half read before the host's write landed carries the previous
 // job's tag, and the job's descriptors are then read again after the word.
 constexpr uint64_t kJobMask = (1ull << 40) - 1;
+constexpr uint64_t kClaimedBit = 1ull << 62;
 constexpr uint64_t kQuitBit = 1ull << 63;
-// word + 31 slots: the mailbox's first 512 bytes, one 16-byte load per lane
-// of wave 0 -- a cfg1 read (16 frames of 4 KiB, and a partial one) fits
-#ifndef KMWS_RESIDENT_POLL_DESCS
-#define KMWS_RESIDENT_POLL_DESCS 31
-#endif
-constexpr int kPollDescs = KMWS_RESIDENT_POLL_DESCS;
+// word + 31 slots: a slot's first 512 bytes, one 16-byte load per lane of
+// wave 0 -- a cfg1 read (16 frames of 4 KiB, and a partial one) fits
+constexpr int kPollDescs = 31;
 static_assert(kPollDescs < 64, "one lane of wave 0 per polled slot");
 constexpr uint64_t kAddrMask = (1ull << 48) - 1;
 constexpr uint32_t kLenMask = (1u << 21) - 1;  // kResMaxBytes fits
@@ -119,13 +137,29 @@ __host__ __device__ __forceinline__ ResDesc untag_desc(ResDesc x)
     x.len &= kLenMask;
     return x;
 }
-struct alignas(256) ResMailbox {
-    uint64_t word;  // job | ndesc << 40 | quit << 63, written last by the host (release)
+
+// Pinned host memory.  Host-written and device-written words sit in different
+// 128-byte lines.
+struct alignas(256) ResSlot {
+    uint64_t word;  // job | ndesc << 40 | claimed << 62 | quit << 63 (host, release)
     uint64_t pad1;
     ResDesc desc[kResMaxDescs];  // desc[i] at 16 + 16 i
-    alignas(128) uint64_t done;    // job number finished (device, release: payloads visible)
-    alignas(128) uint64_t exited;  // incarnation number of the worker that exited
-    alignas(128) uint64_t pad2[16];
+    alignas(128) uint64_t done;    // last job number finished (device, release: payloads visible)
+    uint64_t gone;                 // incarnation whose workgroup of this slot has left (device)
+    alignas(128) uint64_t pad2;
+};
+struct ResMailbox {
+    ResSlot slot[kResSlots];
+    alignas(128) uint64_t exited;  // incarnation whose last workgroup has left (device)
+    alignas(128) uint64_t pad3;
+};
+// Device memory, shared by the grid's workgroups.  Counters and marks are
+// compared with the incarnation number, so nothing is cleared between launches.
+struct ResCtl {
+    uint64_t closing;   // max incarnation that is leaving (idle or lease)
+    uint64_t exits;     // workgroups exited, all incarnations (each adds kResSlots)
+    uint64_t last_act;  // wall clock of the latest job taken in any slot
+    uint64_t pad;
 };
 
 // Loads of host-written words bypass every cache (and are never scalar loads).
@@ -133,10 +167,14 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-// One block, persistent until idle.  `last` = the job number already done when
-// it starts (jobs are numbered from 1); `inc` = this incarnation's number.
-__global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* mb, uint64_t last, uint64_t inc,
+// kResSlots workgroups, persistent until idle; workgroup b serves slot b.
+// `inc` = this incarnation's number (from 1).
+__global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* mb, ResCtl* ctl, uint64_t inc,
                                                                     uint64_t idle_ticks, uint64_t lease_ticks)
 {
     __shared__ ResDesc s_d[kResMaxDescs];
@@ -144,40 +182,61 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     __shared__ uint64_t s_cmd;
     __shared__ uint32_t s_have;  // descriptors taken from the poll
     const int t = threadIdx.x;
+    ResSlot* sl = &mb->slot[blockIdx.x];
     const uint64_t born = wall_clock64();
     // lane l <= kPollDescs of wave 0 polls bytes [16 l, 16 l + 16) of the
-    // mailbox: the job word (lane 0) and descriptor slot l - 1; the other
-    // lanes load lane 0's address (one request)
-    const uint64_t* pw = reinterpret_cast<const uint64_t*>(mb) + 2 * (t <= kPollDescs ? t : 0);
+    // slot: the job word (lane 0) and descriptor slot l - 1; while the slot is
+    // unclaimed every lane loads lane 0's address (one request)
+    const uint64_t* pw0 = &sl->word;
+    const uint64_t* pw = pw0 + 2 * (t <= kPollDescs ? t : 0);
+    uint64_t last = 0, t_act = born;  // (wave 0) job done last; latest activity seen
+    bool full = true;                 // (wave 0) poll the descriptors too
+    if (t < 64) last = ld_sys(&sl->done);
     for (;;) {
         if (t < 64) {  // wave 0, uniform control flow
             uint64_t cmd = 0, v0 = 0, v1 = 0;
-            const uint64_t t0 = wall_clock64();
-            for (;;) {
-                if ((uint64_t)(wall_clock64() - born) > lease_ticks) break;  // a posted job waits for the relaunch
-                v0 = ld_sys(pw);
-                v1 = ld_sys(pw + 1);
+            bool polled_full = false;
+            for (uint32_t it = 0;; ++it) {
+                const uint64_t now = wall_clock64();
+                bool leave = (uint64_t)(now - born) > lease_ticks;  // a posted job waits for the relaunch
+                if (!leave && (it & 3u) == 0) leave = ld_agent(&ctl->closing) >= inc;
+                if (leave) break;
+                const uint64_t* a = full ? pw : pw0;
+                v0 = ld_sys(a);
+                v1 = ld_sys(a + 1);
+                polled_full = full;
                 const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0) |
                                    (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32;
                 // (lane 0's job word; each half through uint32_t: readfirstlane is signed)
-                if (w & kQuitBit) break;
+                if (w & kQuitBit) break;  // this slot only: the rest of the grid serves on
                 if ((w & kJobMask) != last) {
                     cmd = w;
+                    if (t == 0) __hip_atomic_fetch_max(&ctl->last_act, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    t_act = now;
                     break;
                 }
-                if ((uint64_t)(wall_clock64() - t0) > idle_ticks) break;
-                __builtin_amdgcn_s_sleep(2);
+                full = (w & kClaimedBit) != 0;
+                if ((uint64_t)(now - t_act) > idle_ticks) {  // idle here: is every slot idle?
+                    const uint64_t g = ld_agent(&ctl->last_act);
+                    if ((int64_t)(g - t_act) > 0) t_act = g;
+                    if ((uint64_t)(now - t_act) > idle_ticks) {
+                        if (t == 0) __hip_atomic_fetch_max(&ctl->closing, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+                if (full) __builtin_amdgcn_s_sleep(2);
+                else __builtin_amdgcn_s_sleep(127);  // ~4 us: an unclaimed slot gets a job rarely
             }
             uint32_t have = 0;
             if (cmd) {
                 const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
                 const ResDesc x = ResDesc{v0, (uint32_t)v1, (uint32_t)(v1 >> 32)};
-                const bool mine = t >= 1 && t <= (int)nd && t <= kPollDescs;
+                const bool mine = polled_full && t >= 1 && t <= (int)nd && t <= kPollDescs;
                 const bool ok = desc_tagged(x, cmd & kJobMask);
                 if (mine && ok) s_d[t - 1] = untag_desc(x);
                 // every descriptor of the job came with the word: no second round trip
                 const uint64_t bad = __ballot(mine && !ok);
-                have = nd <= (uint32_t)kPollDescs && bad == 0 ? nd : 0u;
+                have = polled_full && nd <= (uint32_t)kPollDescs && bad == 0 ? nd : 0u;
                 // acquire at system scope (the CU's vector L1 and the L2): the
                 // payloads (and descriptors) the host wrote before the job word
                 // are read fresh; the other waves load after the barrier below
@@ -193,8 +252,24 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         if (cmd == 0) break;  // every wave leaves together
         const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
         const uint32_t n = nd < (uint32_t)kResMaxDescs ? nd : (uint32_t)kResMaxDescs;
-        if (s_have == 0 && t < (int)n) s_d[t] = untag_desc(mb->desc[t]);
+        if (s_have == 0 && t < (int)n) {
+            const uint64_t* q = reinterpret_cast<const uint64_t*>(&sl->desc[t]);
+            const uint64_t lo = ld_sys(q), hi = ld_sys(q + 1);  // each half one 8-byte load
+            s_d[t] = untag_desc(ResDesc{lo, (uint32_t)hi, (uint32_t)(hi >> 32)});
+        }
         __syncthreads();
+#ifdef KMWS_TEST_RESIDENT_STALL_KEY
+        // test build only (kuma_amd/build.py): a job whose first payload's key
+        // has these upper 24 bits stalls the workgroup for (key & 0xFF) x 10 ms,
+        // then is dropped if its thread withdrew it meanwhile (the quit bit)
+        if ((s_d[0].key & 0xFFFFFF00u) == (uint32_t)(KMWS_TEST_RESIDENT_STALL_KEY)) {
+            const uint64_t t0 = wall_clock64(), ticks = lease_ticks / kResLeaseUs * 10000u * (s_d[0].key & 0xFFu);
+            while ((uint64_t)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
+            if (t == 0 && (ld_sys(pw0) & kQuitBit)) s_cmd = 0;
+            __syncthreads();
+            if (s_cmd == 0) break;
+        }
+#endif
         if (t == 0) {
             uint32_t w = 0;
             for (uint32_t i = 0; i < n; ++i) {
@@ -250,108 +325,235 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         // every payload byte before it sees `done`
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(&mb->done, cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        last = cmd & kJobMask;
+        if (t == 0) __hip_atomic_store(&sl->done, cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t < 64) last = cmd & kJobMask;
     }
-    if (t == 0) __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) {
+        __hip_atomic_store(&sl->gone, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t before = __hip_atomic_fetch_add(&ctl->exits, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (before + 1 == inc * (uint64_t)kResSlots)  // the grid's last workgroup
+            __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 namespace {
 
 void quit_all_workers();
 
-// One per device, shared by every host thread: a job holds the worker's spin
-// lock from posting its descriptors to seeing it done (jobs take microseconds;
-// the kernel serves one at a time anyway).  Never freed: releasing pinned
-// memory from a static destructor can run after the HIP runtime was torn
-// down.  At process exit an atexit handler -- registered after the HIP
+template <class T>
+T ld_acq(const T* p)
+{
+    return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+}
+
+using Clock = std::chrono::steady_clock;
+
+// One per device, shared by every host thread.  Slots are claimed with one
+// atomic on a bit mask; a job on a slot needs no lock (the slot's thread is
+// its only writer).  launch_mu_ is taken only to relaunch the grid or to
+// withdraw a job no workgroup can take any more.  Never freed: releasing
+// pinned memory from a static destructor can run after the HIP runtime was
+// torn down.  At process exit an atexit handler -- registered after the HIP
 // runtime's own, so it runs before the runtime's teardown -- asks every
-// worker to quit and waits (bounded) until each running kernel has exited:
-// the grid has drained before the process ends.  The idle exit ends a worker
-// nobody feeds.
+// workgroup to quit and waits (bounded) until the grid has exited.
 class ResidentWorker {
 public:
     explicit ResidentWorker(int device) : device_(device) {}
 
-    void lock()
+    // A free slot for the calling thread, or -1 (all taken, or unusable).
+    int claim()
     {
+        if (!usable()) return -1;
+        uint32_t m = ld_acq(&claimed_);
         for (;;) {
-            if (!__atomic_exchange_n(&busy_, true, __ATOMIC_ACQUIRE)) return;
-            while (__atomic_load_n(&busy_, __ATOMIC_RELAXED)) cpu_relax();
+            if (m == 0xFFFFFFFFu >> (32 - kResSlots)) return -1;
+            const int b = __builtin_ctz(~m);
+            if (__atomic_compare_exchange_n(&claimed_, &m, m | (1u << b), false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                // the workgroup polls the descriptors from now on (no job: same number)
+                __atomic_fetch_or(&mb_->slot[b].word, kClaimedBit, __ATOMIC_RELEASE);
+                return b;
+            }
         }
     }
-    void unlock() { __atomic_store_n(&busy_, false, __ATOMIC_RELEASE); }
+    // The thread gives its slot back (thread exit, or it switched the worker
+    // off).  A job still posted on it stays posted and is served.
+    void release(int b)
+    {
+        if (b < 0 || b >= kResSlots || !mb_) return;
+        if (!__atomic_load_n(&exiting_, __ATOMIC_ACQUIRE))
+            __atomic_fetch_and(&mb_->slot[b].word, ~kClaimedBit, __ATOMIC_RELEASE);
+        __atomic_fetch_and(&claimed_, ~(1u << b), __ATOMIC_ACQ_REL);
+    }
 
-    // Ask the kernel to leave at its next poll and wait for it (atexit).
+    // Ask every workgroup to leave at its next poll and wait for the grid (atexit).
     void quit_and_wait()
     {
-        if (!mb_ || !running_) return;
-        __atomic_store_n(&mb_->word, kQuitBit, __ATOMIC_RELEASE);
-        const auto t0 = std::chrono::steady_clock::now();
-        while (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) != inc_ &&
-               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500))
-            cpu_relax();
+        __atomic_store_n(&exiting_, true, __ATOMIC_RELEASE);
+        if (!mb_) return;
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        state_ = -1;  // no relaunch from here on
+        for (int b = 0; b < kResSlots; ++b) __atomic_fetch_or(&mb_->slot[b].word, kQuitBit, __ATOMIC_RELEASE);
+        const uint64_t cur = ld_acq(&inc_);
+        const auto t0 = Clock::now();
+        while (cur && ld_acq(&mb_->exited) != cur && Clock::now() - t0 < std::chrono::milliseconds(500)) cpu_relax();
     }
 
-    // (under the lock) created on first use: a process whose threads all
-    // switched the worker off creates nothing (no stream, no mailbox)
+    // created on first use: a process whose threads all switched the worker
+    // off creates nothing (no stream, no mailbox)
     bool usable()
     {
-        if (state_ == 0) state_ = init() == KMWS_OK ? 1 : -1;
-        return state_ == 1;
+        int s = ld_acq(&state_);
+        if (s == 0) {
+            std::lock_guard<std::mutex> lk(launch_mu_);
+            if (state_ == 0) state_ = init() == KMWS_OK ? 1 : -1;
+            s = state_;
+        }
+        return s == 1;
     }
 
-    // One synchronous job of n <= kResMaxDescs payloads (under the lock).
-    kmws_status run(const ResDesc* d, uint32_t n)
+    // Posts one job of n <= kResMaxDescs payloads on slot b (held by the
+    // calling thread) and returns without waiting; *job = its number.
+    // KMWS_ERR_NOT_SUPPORTED: the slot's previous job is still running, or the
+    // worker cannot be (re)launched -- nothing was posted.
+    kmws_status post(int b, const ResDesc* d, uint32_t n, uint64_t* job)
     {
-        if (n == 0) return KMWS_OK;
-        if (!usable() || n > (uint32_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
-        const uint64_t inc_exited = __atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE);
-        if (!running_ || inc_exited == inc_) {
-            kmws_status st = launch(seq_ & kJobMask);  // every earlier job is done
-            if (st != KMWS_OK) return st;
-        }
-        const uint64_t s = (seq_ + 1) & kJobMask;
+        if (n == 0 || n > (uint32_t)kResMaxDescs || !usable()) return KMWS_ERR_NOT_SUPPORTED;
         for (uint32_t i = 0; i < n; ++i)
             if ((d[i].addr >> 48) != 0 || d[i].len > kLenMask) return KMWS_ERR_NOT_SUPPORTED;
-        // every polled slot is rewritten, so a stale one always carries job s - 1's tag
-        for (uint32_t i = 0; i < n || i < (uint32_t)kPollDescs; ++i)
-            mb_->desc[i] = tag_desc(i < n ? d[i] : ResDesc{0, 0, 0}, s);
-        ++seq_;
-        __atomic_store_n(&mb_->word, s | (uint64_t)n << 40, __ATOMIC_RELEASE);
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t spin = 0;; ++spin) {
-            if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
-            cpu_relax();
-            if ((spin & 255) != 255) continue;
-            if (__atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) == inc_) {
-                // idle or lease exit raced with this job: done is written before exited
-                if (__atomic_load_n(&mb_->done, __ATOMIC_ACQUIRE) == s) break;
-                kmws_status st = launch((s - 1) & kJobMask);  // the new incarnation takes job s
-                if (st != KMWS_OK) return st;
-            }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-                // The job may still run later, so it is not retried (XOR twice is
-                // the identity): the call fails, and this worker is never used
-                // again (later calls launch kernels on their own streams).
-                __atomic_store_n(&mb_->word, kQuitBit, __ATOMIC_RELEASE);
-                state_ = -1;
-                return KMWS_ERR_FAILED;
-            }
+        ResSlot& sl = mb_->slot[b];
+        const uint64_t prev = seq_[b];
+        uint64_t cur = ld_acq(&inc_);
+        if (ld_acq(&sl.done) != prev) {  // busy: the caller launches
+            // (a job a previous holder left posted: a grid that left is relaunched for it)
+            if (cur && ld_acq(&mb_->exited) == cur) (void)relaunch(cur);
+            return KMWS_ERR_NOT_SUPPORTED;
         }
-        ++jobs_;
+        if (cur == 0 || ld_acq(&mb_->exited) == cur) cur = relaunch(cur);
+        if (cur == 0) return KMWS_ERR_NOT_SUPPORTED;
+        const uint64_t s = (prev + 1) & kJobMask;
+        // every polled slot is rewritten, so a stale half always carries job s - 1's tag
+        for (uint32_t i = 0; i < n || i < (uint32_t)kPollDescs; ++i) {
+            const ResDesc x = tag_desc(i < n ? d[i] : ResDesc{0, 0, 0}, s);
+            uint64_t* q = reinterpret_cast<uint64_t*>(&sl.desc[i]);
+            __atomic_store_n(q, x.addr, __ATOMIC_RELAXED);
+            __atomic_store_n(q + 1, (uint64_t)x.len | (uint64_t)x.key << 32, __ATOMIC_RELAXED);
+        }
+        seq_[b] = s;
+        __atomic_fetch_add(&jobs_, 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
+        __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | kClaimedBit, __ATOMIC_RELEASE);
+        *job = s;
         return KMWS_OK;
     }
 
-    uint64_t jobs() const { return jobs_; }
-    uint64_t launches() const { return inc_; }
-    int running()
+    // 1 when job s of slot b is done, 0 while it runs (relaunching a grid that
+    // left before taking it), KMWS_ERR_NOT_SUPPORTED when it was withdrawn
+    // (never run: the caller launches it).
+    int test(int b, uint64_t s)
     {
-        return running_ && __atomic_load_n(&mb_->exited, __ATOMIC_ACQUIRE) != inc_ ? 1 : 0;
+        ResSlot& sl = mb_->slot[b];
+        if (ld_acq(&sl.done) == s) return 1;
+        const uint64_t cur = ld_acq(&inc_);
+        if (ld_acq(&mb_->exited) == cur) {
+            if (ld_acq(&sl.done) == s) return 1;
+            if (relaunch(cur) == 0 && withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
+        }
+        return 0;
+    }
+
+    // Waits for job s of slot b.  KMWS_OK: done.  KMWS_ERR_NOT_SUPPORTED:
+    // withdrawn without having run (payloads untouched; the caller launches).
+    // KMWS_ERR_TIMEOUT: the workgroup holding it neither finished nor left
+    // within the bounds -- the device may still write its payloads.
+    kmws_status wait(int b, uint64_t s)
+    {
+        ResSlot& sl = mb_->slot[b];
+        const auto t0 = Clock::now();
+        Clock::time_point orphan{};
+        for (uint32_t spin = 0;; ++spin) {
+            if (ld_acq(&sl.done) == s) return KMWS_OK;
+            cpu_relax();
+            if ((spin & 255) != 255) continue;
+            const uint64_t cur = ld_acq(&inc_);
+            if (ld_acq(&mb_->exited) == cur) {  // the whole grid left: relaunch (the new one takes job s)
+                if (ld_acq(&sl.done) == s) return KMWS_OK;
+                if (relaunch(cur) == 0) {
+                    if (withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
+                    continue;
+                }
+                orphan = Clock::time_point{};
+            } else if (ld_acq(&sl.gone) == cur) {  // this slot's workgroup left, others run on
+                if (ld_acq(&sl.done) == s) return KMWS_OK;
+                const auto now = Clock::now();
+                if (orphan == Clock::time_point{}) orphan = now;
+                else if (now - orphan > std::chrono::microseconds(kResOrphanUs) && withdraw(b, s, cur))
+                    return KMWS_ERR_NOT_SUPPORTED;
+            } else {
+                orphan = Clock::time_point{};
+            }
+            if (Clock::now() - t0 > std::chrono::milliseconds(KMWS_RESIDENT_TIMEOUT_MS)) return timed_out(b, s);
+        }
+    }
+
+    uint64_t jobs() const { return ld_acq(&jobs_); }
+    uint64_t launches() const { return ld_acq(&inc_); }
+    uint64_t timeouts() const { return ld_acq(&timeouts_); }
+    uint64_t withdrawn() const { return ld_acq(&withdrawn_); }
+    int claimed() const { return __builtin_popcount(ld_acq(&claimed_)); }
+    int running() const
+    {
+        const uint64_t cur = ld_acq(&inc_);
+        return mb_ && cur && ld_acq(&mb_->exited) != cur ? 1 : 0;
     }
 
 private:
-    kmws_status init()
+    // Takes job s of slot b back if no workgroup can take it any more: the
+    // grid `cur` is still the latest (no relaunch can start while launch_mu_
+    // is held) and its workgroup for b has left.  The slot's word returns to
+    // the previous job number (the quit bit cleared), so no later incarnation
+    // runs it.  False: it was done after all, or a newer grid will take it.
+    bool withdraw(int b, uint64_t s, uint64_t cur)
+    {
+        ResSlot& sl = mb_->slot[b];
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        if (ld_acq(&inc_) != cur || ld_acq(&sl.done) == s) return false;
+        if (ld_acq(&sl.gone) != cur && ld_acq(&mb_->exited) != cur) return false;
+        const uint64_t prev = (s - 1) & kJobMask;
+        seq_[b] = prev;
+        __atomic_store_n(&sl.word, prev | kClaimedBit, __ATOMIC_RELEASE);
+        __atomic_fetch_add(&withdrawn_, 1, __ATOMIC_RELAXED);
+        __atomic_fetch_sub(&jobs_, 1, __ATOMIC_RELAXED);
+        return true;
+    }
+
+    // Past the timeout: the quit bit asks slot b's workgroup to leave (it may
+    // be inside the job, or stuck); wait, bounded, until it has.
+    kmws_status timed_out(int b, uint64_t s)
+    {
+        ResSlot& sl = mb_->slot[b];
+        __atomic_fetch_add(&timeouts_, 1, __ATOMIC_RELAXED);
+        __atomic_fetch_or(&sl.word, kQuitBit, __ATOMIC_RELEASE);
+        const auto t0 = Clock::now();
+        for (uint32_t spin = 0;; ++spin) {
+            if (ld_acq(&sl.done) == s) {
+                std::lock_guard<std::mutex> lk(launch_mu_);
+                __atomic_fetch_and(&sl.word, ~kQuitBit, __ATOMIC_RELEASE);
+                return KMWS_OK;
+            }
+            cpu_relax();
+            if ((spin & 255) != 255) continue;
+            const uint64_t cur = ld_acq(&inc_);
+            if ((ld_acq(&sl.gone) == cur || ld_acq(&mb_->exited) == cur) && withdraw(b, s, cur))
+                return KMWS_ERR_NOT_SUPPORTED;  // it left without running the job
+            if (Clock::now() - t0 > std::chrono::milliseconds(KMWS_RESIDENT_DRAIN_MS)) break;
+        }
+        // still held by a workgroup that does not leave: the payloads stay the
+        // device's, and no job is posted on this device's worker again
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        state_ = -1;
+        return KMWS_ERR_TIMEOUT;
+    }
+
+    kmws_status init()  // under launch_mu_
     {
         if (device_ < 0 || kmws_device_count() <= device_) return KMWS_ERR_NOT_SUPPORTED;
         DevGuard g(device_);
@@ -364,6 +566,11 @@ private:
         std::memset(static_cast<void*>(mb_), 0, sizeof(ResMailbox));
         dmb_ = static_cast<ResMailbox*>(device_view(mb_));
         if (!dmb_) return KMWS_ERR_FAILED;
+        if (hipMalloc(reinterpret_cast<void**>(&dctl_), sizeof(ResCtl)) != hipSuccess ||
+            hipMemset(dctl_, 0, sizeof(ResCtl)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipGetLastError();
+            return KMWS_ERR_FAILED;
+        }
         // A non-blocking stream: the legacy default stream (torch's current stream
         // unless the caller picked another) waits for every blocking stream's
         // work, which would include this kernel -- measured: a kernel on the null
@@ -393,29 +600,40 @@ private:
         return KMWS_OK;
     }
 
-    kmws_status launch(uint64_t last)
+    // Launches the next incarnation once `seen` (0: none yet) has left
+    // entirely; returns the incarnation now serving, or 0 if the worker is
+    // unusable (nothing launched).
+    uint64_t relaunch(uint64_t seen)
     {
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        if (state_ != 1) return 0;
+        const uint64_t cur = inc_;
+        if (cur != seen) return cur;                                   // another thread relaunched
+        if (cur != 0 && ld_acq(&mb_->exited) != cur) return cur;      // still running
         DevGuard g(device_);
-        ++inc_;
-        hipLaunchKernelGGL(resident_unmask_kernel, dim3(1), dim3(kResBlock), 0, stream_, dmb_, last, inc_,
+        hipLaunchKernelGGL(resident_unmask_kernel, dim3(kResSlots), dim3(kResBlock), 0, stream_, dmb_, dctl_, cur + 1,
                            idle_ticks_, lease_ticks_);
         if (hipGetLastError() != hipSuccess) {
             state_ = -1;
-            return KMWS_ERR_FAILED;
+            return 0;
         }
-        running_ = true;
-        return KMWS_OK;
+        __atomic_store_n(&inc_, cur + 1, __ATOMIC_RELEASE);
+        return cur + 1;
     }
 
     int device_;
-    bool busy_ = false;  // the spin lock
-    int state_ = 0;      // 0 untried, 1 ready, -1 unusable
-    bool running_ = false;
+    std::mutex launch_mu_;
+    int state_ = 0;  // 0 untried, 1 ready, -1 unusable
+    bool exiting_ = false;
+    uint32_t claimed_ = 0;  // bit b: slot b held by a thread
     ResMailbox* mb_ = nullptr;
     ResMailbox* dmb_ = nullptr;
+    ResCtl* dctl_ = nullptr;
     hipStream_t stream_ = nullptr;
     uint64_t idle_ticks_ = 0, lease_ticks_ = 0;
-    uint64_t seq_ = 0, inc_ = 0, jobs_ = 0;
+    uint64_t inc_ = 0;  // latest incarnation launched
+    uint64_t seq_[kResSlots] = {};  // last job number posted per slot (by its holder)
+    uint64_t jobs_ = 0, timeouts_ = 0, withdrawn_ = 0;
 };
 
 // Every worker of the process (for the exit handler); never freed.
@@ -449,40 +667,94 @@ ResidentWorker* worker(int device)
     return w;
 }
 
-// kmws_resident_enable is per calling thread: a thread that switched the
-// worker off launches its jobs (the A/B of the worker), others keep it.
-thread_local uint64_t t_off_mask = 0;  // bit d: off for device d on this thread
-bool off_here(int device) { return device >= 0 && device < kMaxDevices && ((t_off_mask >> device) & 1u); }
+// The calling thread's slots, one per device (-1: none held; -2: its job
+// timed out, the slot is never given back), released when the thread exits.
+// kmws_resident_enable(0) makes the thread's calls launch instead (the A/B of
+// the worker) and gives its slot back.
+struct ThreadSlots {
+    int8_t slot[kMaxDevices];
+    uint64_t off_mask = 0;  // bit d: worker off for device d on this thread
+    ThreadSlots() { std::memset(slot, -1, sizeof slot); }
+    ~ThreadSlots()
+    {
+        for (int d = 0; d < kMaxDevices; ++d)
+            if (slot[d] >= 0)
+                if (ResidentWorker* w = __atomic_load_n(&g_by_dev[d], __ATOMIC_ACQUIRE)) w->release(slot[d]);
+    }
+};
+thread_local ThreadSlots t_slots;
+
+// The calling thread's slot on `device` (claimed on first use), or -1.
+int thread_slot(int device, ResidentWorker** wout)
+{
+    if (device < 0 || device >= kMaxDevices || ((t_slots.off_mask >> device) & 1u)) return -1;
+    ResidentWorker* w = worker(device);
+    if (!w) return -1;
+    *wout = w;
+    int b = t_slots.slot[device];
+    if (b == -1) {
+        b = w->claim();
+        if (b >= 0) t_slots.slot[device] = (int8_t)b;
+    }
+    return b;
+}
 
 }  // namespace
 
-// Synchronous unmask of host payloads (device-visible views of pinned memory)
-// through the device's resident worker.  KMWS_ERR_NOT_SUPPORTED: the job does
-// not fit a worker job (more than kResMaxDescs payloads or kResMaxBytes bytes),
-// the calling thread switched the worker off, or it is unusable; the caller
-// launches.
-kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
-                            const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2)
+// Posts the unmask of descs[0..n) over dev_base and descs2[0..n2) over
+// dev_base2 (device views of pinned host memory, offsets relative to them) on
+// the calling thread's slot; see kmws_common.hpp.
+kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
+                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job)
 {
-    if (n + n2 > (size_t)kResMaxDescs || off_here(device)) return KMWS_ERR_NOT_SUPPORTED;
-    ResidentWorker* w = worker(device);
-    if (!w) return KMWS_ERR_NOT_SUPPORTED;
-    ResDesc job[kResMaxDescs];
+    if (n + n2 == 0 || n + n2 > (size_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
+    ResidentWorker* w = nullptr;
+    const int b = thread_slot(device, &w);
+    if (b < 0) return KMWS_ERR_NOT_SUPPORTED;
+    ResDesc d[kResMaxDescs];
     uint64_t bytes = 0;
     size_t k = 0;
     for (size_t i = 0; i < n; ++i, ++k) {
-        job[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base + descs[i].off), descs[i].len, descs[i].key};
+        d[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base + descs[i].off), descs[i].len, descs[i].key};
         bytes += descs[i].len;
     }
     for (size_t i = 0; i < n2; ++i, ++k) {
-        job[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base2 + descs2[i].off), descs2[i].len, descs2[i].key};
+        d[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base2 + descs2[i].off), descs2[i].len, descs2[i].key};
         bytes += descs2[i].len;
     }
     if (bytes > kResMaxBytes) return KMWS_ERR_NOT_SUPPORTED;
-    w->lock();
-    const kmws_status st = w->run(job, (uint32_t)k);
-    w->unlock();
+    uint64_t s = 0;
+    const kmws_status st = w->post(b, d, (uint32_t)k, &s);
+    if (st != KMWS_OK) return st;
+    job->device = device;
+    job->slot = b;
+    job->seq = s;
+    return KMWS_OK;
+}
+
+int resident_test(const ResidentJob& job)
+{
+    ResidentWorker* w = worker(job.device);
+    return w ? w->test(job.slot, job.seq) : KMWS_ERR_INVALID_PARAM;
+}
+
+kmws_status resident_wait(const ResidentJob& job)
+{
+    ResidentWorker* w = worker(job.device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    const kmws_status st = w->wait(job.slot, job.seq);
+    if (st == KMWS_ERR_TIMEOUT && job.device >= 0 && job.device < kMaxDevices &&
+        t_slots.slot[job.device] == job.slot)
+        t_slots.slot[job.device] = -2;  // the slot stays the device's
     return st;
+}
+
+kmws_status resident_unmask(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
+                            const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2)
+{
+    ResidentJob job;
+    const kmws_status st = resident_post(device, descs, dev_base, n, descs2, dev_base2, n2, &job);
+    return st != KMWS_OK ? st : resident_wait(job);
 }
 
 }  // namespace kmws
@@ -492,8 +764,17 @@ extern "C" {
 kmws_status kmws_resident_enable(int device, int on)
 {
     if (device < 0 || device >= kmws::kMaxDevices) return KMWS_ERR_INVALID_PARAM;
-    if (on) kmws::t_off_mask &= ~(1ull << device);
-    else kmws::t_off_mask |= 1ull << device;
+    kmws::ThreadSlots& ts = kmws::t_slots;
+    if (on) {
+        ts.off_mask &= ~(1ull << device);
+    } else {
+        ts.off_mask |= 1ull << device;
+        if (ts.slot[device] >= 0) {
+            if (kmws::ResidentWorker* w = __atomic_load_n(&kmws::g_by_dev[device], __ATOMIC_ACQUIRE))
+                w->release(ts.slot[device]);
+            ts.slot[device] = -1;
+        }
+    }
     return KMWS_OK;
 }
 
@@ -501,11 +782,21 @@ kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, i
 {
     kmws::ResidentWorker* w = kmws::worker(device);
     if (!w) return KMWS_ERR_INVALID_PARAM;
-    w->lock();
     if (jobs) *jobs = w->jobs();
     if (launches) *launches = w->launches();
     if (running) *running = w->running();
-    w->unlock();
+    return KMWS_OK;
+}
+
+kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_claimed, uint64_t* timeouts,
+                                   uint64_t* withdrawn)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    if (thread_slot) *thread_slot = kmws::t_slots.slot[device] >= 0 ? kmws::t_slots.slot[device] : -1;
+    if (slots_claimed) *slots_claimed = w->claimed();
+    if (timeouts) *timeouts = w->timeouts();
+    if (withdrawn) *withdrawn = w->withdrawn();
     return KMWS_OK;
 }
 

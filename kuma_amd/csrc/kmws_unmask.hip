@@ -18,13 +18,6 @@
 #include "kmws_common.hpp"
 #include "kmws_frame_parse.hpp"
 
-// Uncapped split grids (batches of frames shorter than a tile, the LDS-staged
-// path) load the tile's descriptors before its payload: cfg4's in-place unmask
-// 80.3-80.4 -> 81.7-82.2 % (profiles/r02bt_unmask_desc_prefetch_ab.txt).  0 = off.
-#ifndef KMWS_UNMASK_PRE
-#define KMWS_UNMASK_PRE 1
-#endif
-
 namespace kmws {
 
 // Payload store of a tile word: non-temporal (streams past the L2; the
@@ -341,10 +334,11 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
     }
     const uint64_t lo = (uint64_t)tile * Cfg::kTile;
     u32x4 v[V];
-#if KMWS_UNMASK_PRE
     if constexpr (!TWO) {
         // the tile's descriptors first: their wait then counts only them, not the
-        // payload loads issued after them (vmcnt is one in-order queue)
+        // payload loads issued after them (vmcnt is one in-order queue; cfg4's
+        // in-place unmask 80.3-80.4 -> 81.7-82.2 %,
+        // profiles/r02bt_unmask_desc_prefetch_ab.txt)
         const uint32_t f = map[tile], fl = map[tile + 1];
         const uint32_t fi = f + threadIdx.x;
         u32x4 pre = u32x4{0, 0, 0, 0};
@@ -355,7 +349,6 @@ __global__ void __launch_bounds__(kBlock) unmask_split_kernel(uint8_t* __restric
                                       s_key, &pre);
         return;
     }
-#endif
     load_tile<V, true>(base, lo, lo + Cfg::kTile, v);
     __builtin_amdgcn_sched_barrier(0);
     // the status is read after the payload loads: its latency hides under theirs
@@ -485,11 +478,8 @@ using ProdCfg = UnmaskCfg<kUnmaskV>;
 // the 64 GiB batch at 84.5-84.8 % of peak against 82.4-82.9 % with the 6 the
 // registers allow, 3 blocks at 83.4 %, 1 block at 65-75 %
 // (profiles/r02ag_unmask_occupancy.txt).  The cap is dynamic LDS the kernel does
-// not use: a block asks for just over a third of the CU's LDS.  Compile-time
-// (a tuning build may define another value; 0 = no cap).
-#ifndef KMWS_UNMASK_BLOCKS_PER_CU
-#define KMWS_UNMASK_BLOCKS_PER_CU 2
-#endif
+// not use: a block asks for just over a third of the CU's LDS.
+constexpr unsigned kUnmaskBlocksPerCu = 2;
 constexpr uint32_t kUnmaskStaticLds = ProdCfg::kCap * (8 + 8 + 4);  // s_off, s_end, s_key
 
 static unsigned unmask_lds_pad_device()
@@ -501,10 +491,10 @@ static unsigned unmask_lds_pad_device()
     if (dev != dev_cached) {
         int lds = 0;
         pad = 0;
-        if (KMWS_UNMASK_BLOCKS_PER_CU > 0 &&
+        if (
             hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) == hipSuccess &&
             lds > 0) {
-            const unsigned per_block = (unsigned)lds / (unsigned)(KMWS_UNMASK_BLOCKS_PER_CU + 1) + 1;  // one more does not fit
+            const unsigned per_block = (unsigned)lds / (kUnmaskBlocksPerCu + 1) + 1;  // one more does not fit
             pad = per_block > kUnmaskStaticLds ? per_block - kUnmaskStaticLds : 0u;
         }
         dev_cached = dev;

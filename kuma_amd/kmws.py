@@ -17,7 +17,7 @@ from typing import Callable, List, Optional, Sequence
 from . import build as _build
 
 # ---- constants (include/kmws_gpu.h) ----
-OK, ERR_FAILED, ERR_INVALID_STATE, ERR_INVALID_PARAM = 0, -1, -7, -8
+OK, ERR_FAILED, ERR_TIMEOUT, ERR_INVALID_STATE, ERR_INVALID_PARAM = 0, -1, -6, -7, -8
 ERR_BUFFER_TOO_SMALL, ERR_BUFFER_TOO_LONG, ERR_NOT_SUPPORTED = -17, -18, -19
 CLIENT, SERVER = 0, 1
 OP_CONTINUE, OP_TEXT, OP_BINARY, OP_CLOSE, OP_PING, OP_PONG = 0, 1, 2, 8, 9, 10
@@ -48,7 +48,7 @@ EXPORTS = [
 #: every function include/kmws_bench.h declares (bench / test support, same library)
 BENCH_EXPORTS = [
     "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
-    "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info",
+    "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info", "kmws_resident_counters",
 ]
 
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
@@ -100,7 +100,13 @@ def lib() -> C.CDLL:
                 raise RuntimeError(f"kmws: {path} missing and cannot be built: {e}") from e
     if not os.path.exists(path):
         raise RuntimeError(f"kmws: HIP library {path} not built (run __graft_entry__.build())")
-    L = C.CDLL(path)
+    _lib = bind(C.CDLL(path))
+    return _lib
+
+
+def bind(L: C.CDLL) -> C.CDLL:
+    """Sets the C signatures on a loaded libkmws_gpu.so (the product library, or
+    a test variant a test loads by path)."""
     vp, u8p, sz, u32, u64, i32 = C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int
     sig = {
         "kmws_encode_header": (i32, [C.POINTER(FrameHdr), u8p]),
@@ -128,6 +134,8 @@ def lib() -> C.CDLL:
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
         "kmws_resident_enable": (i32, [i32, i32]),
         "kmws_resident_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+        "kmws_resident_counters": (i32, [i32, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint64)]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
         "kmws_encode_batch": (i32, [u8p, vp, vp, u32, u8p, u64, vp, vp, sz, vp]),
         "kmws_unpack_workspace_size": (sz, []),
@@ -168,7 +176,6 @@ def lib() -> C.CDLL:
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
-    _lib = L
     return L
 
 
@@ -323,12 +330,20 @@ class WSHandler:
     encodeFrameHeader = staticmethod(encode_frame_header)
 
 
-def resident_info(device: int = 0) -> dict:
-    """kmws_resident_info of the device's resident worker (shared by the process's threads)."""
+def resident_info(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
+    """kmws_resident_info of the device's resident worker (one grid per device,
+    a mailbox slot per loop thread), plus kmws_resident_counters: the calling
+    thread's slot (-1: none), slots held, timed-out and withdrawn jobs.  `L`: a
+    test variant of the library (bind()), else the product library."""
+    L = L or lib()
     jobs, launches, running = C.c_uint64(0), C.c_uint64(0), C.c_int(0)
-    _check(lib().kmws_resident_info(device, C.byref(jobs), C.byref(launches), C.byref(running)),
-           "kmws_resident_info")
-    return {"jobs": jobs.value, "launches": launches.value, "running": bool(running.value)}
+    _check(L.kmws_resident_info(device, C.byref(jobs), C.byref(launches), C.byref(running)), "kmws_resident_info")
+    slot, claimed, tmo, wd = C.c_int(0), C.c_int(0), C.c_uint64(0), C.c_uint64(0)
+    _check(L.kmws_resident_counters(device, C.byref(slot), C.byref(claimed), C.byref(tmo), C.byref(wd)),
+           "kmws_resident_counters")
+    return {"jobs": jobs.value, "launches": launches.value, "running": bool(running.value),
+            "thread_slot": slot.value, "slots_claimed": claimed.value, "timeouts": tmo.value,
+            "withdrawn": wd.value}
 
 
 def resident_enable(on: bool, device: int = 0) -> None:
@@ -336,14 +351,15 @@ def resident_enable(on: bool, device: int = 0) -> None:
     _check(lib().kmws_resident_enable(device, int(bool(on))), "kmws_resident_enable")
 
 
-def handle_data_mask(key: bytes, segments, device: int = 0) -> None:
-    """WSHandler::handleDataMask over a chain of bytearrays (in place, GPU)."""
+def handle_data_mask(key: bytes, segments, device: int = 0, L: Optional[C.CDLL] = None) -> None:
+    """WSHandler::handleDataMask over a chain of bytearrays (in place, GPU).
+    `L`: a test variant of the library (bind()), else the product library."""
     segs = list(segments)
     bufs = [(C.c_uint8 * max(1, len(s))).from_buffer(s) if len(s) else (C.c_uint8 * 1)() for s in segs]
     ptrs = (C.c_void_p * max(1, len(segs)))(*[C.addressof(b) for b in bufs])
     lens = (C.c_size_t * max(1, len(segs)))(*[len(s) for s in segs])
     k = (C.c_uint8 * 4).from_buffer_copy(bytes(key))
-    _check(lib().kmws_mask_host_chain(k, ptrs, lens, len(segs), device), "kmws_mask_host_chain")
+    _check((L or lib()).kmws_mask_host_chain(k, ptrs, lens, len(segs), device), "kmws_mask_host_chain")
 
 
 class RxBatch:
@@ -656,8 +672,24 @@ def copy_workspace_size(n: int, dst_cap: int) -> int:
     return lib().kmws_copy_workspace_size(n, dst_cap)
 
 
-def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None) -> None:
-    """kmws_encode_batch: descs (n,2) int64, flags int16 (n,), wire_off int64 (n+1,)."""
+def _raise_on_status(ws: "Workspace", stream, what: str, out: str) -> None:
+    """The synchronizing check of check=True: reads the workspace status back
+    (a stream synchronize) and raises KmwsError (.ws_status) when it is nonzero
+    -- a bad descriptor or batch (1), a header error (2), or a scan look-back
+    that timed out (4): `out` is then invalid.  Skipped inside a graph capture."""
+    if _capturing():
+        return
+    st = ws.status(stream)
+    if st:
+        e = KmwsError(ERR_FAILED, f"{what} (workspace status {st}: {out} invalid)")
+        e.ws_status = st
+        raise e
+
+
+def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None, check: bool = False) -> None:
+    """kmws_encode_batch: descs (n,2) int64, flags int16 (n,), wire_off int64 (n+1,).
+    Stream-ordered; check=True synchronizes and raises on a nonzero workspace
+    status (wire_off and dst are valid only when it is 0)."""
     n = _check_descs(descs)
     dev = descs.device
     _check_tensor(src, "src", 1, dev)
@@ -668,6 +700,8 @@ def encode_batch(src, descs, flags, dst, wire_off, ws: Workspace, stream=None) -
     _check(lib().kmws_encode_batch(src.data_ptr(), descs.data_ptr(), flags.data_ptr(), n,
                                    dst.data_ptr(), dst.numel(), wire_off.data_ptr(), ws.ptr, ws.nbytes,
                                    _stream_handle(stream)), "kmws_encode_batch")
+    if check and n:
+        _raise_on_status(ws, stream, "kmws_encode_batch", "wire_off")
 
 
 def pack_headers_workspace_size(n: int) -> int:
@@ -680,13 +714,14 @@ def _capturing() -> bool:
 
 
 def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Workspace] = None,
-                 stream=None, check: bool = True) -> None:
-    """kmws_pack_headers: headers only, frame i's into the 16-B slot hdr[16 i:]
-    (uint8 device tensor of >= 16 n bytes), lengths into hdr_len (uint8, n),
-    wire offsets into wire_off (int64, n+1; needs ws).  With wire_off and
-    `check` (outside a graph capture) the workspace status is read back
-    (synchronizing) and a nonzero one -- a bad descriptor, or the look-back
-    timeout that leaves wire_off invalid -- raises KmwsError."""
+                 stream=None, check: bool = False) -> None:
+    """kmws_pack_headers (stream-ordered; check=True synchronizes): headers
+    only, frame i's into the 16-B slot hdr[16 i:] (uint8 device tensor of >=
+    16 n bytes), lengths into hdr_len (uint8, n), wire offsets into wire_off
+    (int64, n+1; needs ws; valid only when the workspace status is 0).  With
+    wire_off and check=True (outside a graph capture) the status is read back
+    and a nonzero one -- a bad descriptor, or the look-back timeout that leaves
+    wire_off invalid -- raises KmwsError."""
     n = _check_descs(descs)
     dev = descs.device
     _check_tensor(flags, "flags", 2, dev, n)
@@ -702,12 +737,8 @@ def pack_headers(descs, flags, hdr, hdr_len=None, wire_off=None, ws: Optional[Wo
                                    wire_off.data_ptr() if wire_off is not None else None,
                                    ws.ptr if ws is not None else None, ws.nbytes if ws is not None else 0,
                                    _stream_handle(stream)), "kmws_pack_headers")
-    if check and wire_off is not None and ws is not None and n and not _capturing():
-        st = ws.status(stream)
-        if st:
-            e = KmwsError(ERR_FAILED, f"kmws_pack_headers (workspace status {st}: wire_off invalid)")
-            e.ws_status = st
-            raise e
+    if check and wire_off is not None and ws is not None and n:
+        _raise_on_status(ws, stream, "kmws_pack_headers", "wire_off")
 
 
 def find_headers_streams(wire, stream_off, cap: int, wire_len: Optional[int] = None, stream=None):
@@ -740,7 +771,9 @@ def unpack_headers(wire, hdr_off, mode: int, out_desc, out_flags, out_err, ws: W
                                      ws.ptr, ws.nbytes, _stream_handle(stream)), "kmws_unpack_headers")
 
 
-def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
+def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None, check: bool = False) -> None:
+    """kmws_gather_unmask (stream-ordered): dst_off and dst are valid only when
+    the workspace status is 0; check=True synchronizes and raises otherwise."""
     n = _check_descs(descs)
     dev = descs.device
     _check_tensor(src, "src", 1, dev)
@@ -750,6 +783,8 @@ def gather_unmask(src, descs, dst, dst_off, ws: Workspace, stream=None) -> None:
     _check(lib().kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), n, dst.data_ptr(),
                                     dst.numel(), dst_off.data_ptr(), ws.ptr, ws.nbytes,
                                     _stream_handle(stream)), "kmws_gather_unmask")
+    if check and n:
+        _raise_on_status(ws, stream, "kmws_gather_unmask", "dst_off")
 
 
 def _opt(t):

@@ -23,8 +23,10 @@
 //        frames queued on the loop thread's kmws::RxLoop, whose posted task
 //        submits the iteration's unmask and delivers finished generations at the
 //        next iterations (asynchronous, the GPU round trip overlaps the reads);
-//        the client submits each iteration's masks (kmws_tx_batch_submit) and
-//        writes the previous iteration's frames while they run (two send slots).
+//        the client sends through its loop thread's kmws::TxLoop (sendWsFrame's
+//        replacement: header packed and payload copied into the pinned send
+//        ring at send, one mask job per iteration, frames written by the posted
+//        task once their generation completed, two generations in flight).
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
@@ -152,6 +154,7 @@ struct LoopObjs {
     kmws_tx_batch* tx = nullptr;
     uint8_t* sring = nullptr;
     kmws::RxLoop* rxloop = nullptr;  // adapter mode: the server loop's RxLoop (owns its own batch)
+    kmws::TxLoop* txloop = nullptr;  // adapter mode: the client loop's TxLoop (owns its batch and ring)
 };
 
 // One connection: returns seconds from the first send to the last delivered frame.
@@ -319,33 +322,22 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     std::vector<iovec> iov;
     const auto t0 = std::chrono::steady_clock::now();
     if (adapter) {
-        // two send slots: iteration k fills and submits slot k % 2, then writes
-        // iteration k - 1 once its masks completed
-        std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hd[2] = {hdrs, hdrs};
-        std::vector<int> hl[2] = {hlen, hlen};
-        int64_t ticket[2] = {0, 0};
-        int count[2] = {0, 0};
-        auto write_slot = [&](int sl) {
-            double tt = now_s();
-            if (kmws_tx_batch_poll(tx, ticket[sl], 1) != 1) std::exit(7);
-            g_t.tx_flush += now_s() - tt;
-            iov.clear();
-            uint8_t* base = sring + (size_t)sl * kGroup * kLen;
-            for (int j = 0; j < count[sl]; ++j) {
-                iov.push_back(iovec{hd[sl][j].data(), (size_t)hl[sl][j]});
-                iov.push_back(iovec{base + (size_t)j * kLen, kLen});
-            }
-            tt = now_s();
+        // the client loop thread: its TxLoop (the posted task masks the
+        // iteration's sends with one GPU job and writes finished generations)
+        std::vector<kmws::TxLoop::Task> ctasks;
+        kmws::TxLoop& txl = *lo.txloop;
+        txl.setPoster([&ctasks](kmws::TxLoop::Task t) { ctasks.push_back(std::move(t)); });
+        kmws::TxLoop::Conn* conn = txl.open([&](const iovec* v, int cnt) {  // ws_conn_->send(iovs, cnt)
+            const double tt = now_s();
+            iov.assign(v, v + cnt);
             send_all(fd, iov);
             g_t.writev += now_s() - tt;
-        };
-        int k = 0;
-        for (int g0 = 0; g0 < kFrames; g0 += kGroup, ++k) {
-            const int sl = k & 1, ng = std::min(kGroup, kFrames - g0);
-            uint8_t* base = sring + (size_t)sl * kGroup * kLen;
-            std::memcpy(base, e.plain.data() + (size_t)g0 * kLen, (size_t)ng * kLen);
+            return 0;
+        });
+        for (int g0 = 0; g0 < kFrames; g0 += kGroup) {
+            // one loop iteration: the application's sends (sendWsFrame), then the posted tasks
+            const int ng = std::min(kGroup, kFrames - g0);
             for (int j = 0; j < ng; ++j) {
-                uint8_t* p = base + (size_t)j * kLen;
                 const uint32_t key = keys[g0 + j];
                 kmws_frame_hdr h;
                 std::memset(&h, 0, sizeof h);
@@ -353,17 +345,18 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 h.opcode = KMWS_OP_TEXT;
                 h.mask = 1;
                 std::memcpy(h.maskey, &key, 4);
-                size_t len = kLen;
-                hl[sl][j] = kmws_tx_batch_add(tx, &h, &p, &len, 1, hd[sl][j].data());
+                if (txl.send(conn, h, e.plain.data() + (size_t)(g0 + j) * kLen, kLen) < 0) std::exit(7);
             }
-            double tt = now_s();
-            ticket[sl] = kmws_tx_batch_submit(tx);
-            g_t.tx_flush += now_s() - tt;
-            if (ticket[sl] <= 0) std::exit(7);
-            count[sl] = ng;
-            if (k > 0) write_slot(sl ^ 1);
+            const double tt = now_s(), w0 = g_t.writev;
+            std::vector<kmws::TxLoop::Task> now;
+            now.swap(ctasks);
+            for (auto& t : now) t();
+            if (txl.lastResult() < 0 || conn->lastResult() < 0) std::exit(7);
+            g_t.tx_flush += now_s() - tt - (g_t.writev - w0);
         }
-        if (k > 0) write_slot((k - 1) & 1);
+        const double tt = now_s(), w0 = g_t.writev;
+        if (txl.close(conn) < 0) std::exit(7);  // the last generations: masked and written
+        g_t.tx_flush += now_s() - tt - (g_t.writev - w0);
     }
     for (int g0 = 0; g0 < kFrames && !adapter; g0 += kGroup) {
         const int ng = std::min(kGroup, kFrames - g0);
@@ -462,6 +455,8 @@ int main(int argc, char** argv)
         if (adapter) {
             lo.rxloop = new kmws::RxLoop(nullptr, 0);
             if (!lo.rxloop->valid() || lo.rxloop->attachRing(lo.rring, kRing) != KMWS_OK) return 3;
+            lo.txloop = new kmws::TxLoop(nullptr, 0);
+            if (!lo.txloop->valid()) return 3;
         } else if (kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK) {
             return 3;
         }
@@ -475,6 +470,7 @@ int main(int argc, char** argv)
     }
     if (gpu) {
         delete lo.rxloop;
+        delete lo.txloop;
         kmws_rx_batch_destroy(lo.rx);
         kmws_tx_batch_destroy(lo.tx);
         kmws_host_free(lo.rring);

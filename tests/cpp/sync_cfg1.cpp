@@ -11,6 +11,13 @@
 //                     staging copy (kmws_decoder_set_in_place(0)): no copy back;
 //             launch  the resident form with the worker switched off (a kernel
 //                     launch and an event wait per read: round 3's form).
+//   decode_sync_threads  the same decode on T = 1, 2, 4, 8 loop threads at
+//           once (kuma runs 5-10 loop threads, test/server/main.cpp:22,
+//           test/client/main.cpp:20), each with its own handler and read
+//           buffer, `passes` passes of the stream each; aggregate GiB/s over
+//           the wall time of all threads (the copy of each read into the
+//           buffer is timed here, for every codec alike).  The resident form
+//           gives each thread its own slot of the device's resident grid.
 //   mask    WSHandler::handleDataMask(key, data, len) once per send
 //           (WebSocketImpl.cpp:388), 1 KiB, 4 KiB and 64 KiB payloads in a
 //           pageable buffer: the oracle's byte loop vs
@@ -23,12 +30,16 @@
 //
 // usage: sync_cfg1 [reps]
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kmws_bench.h"
@@ -114,6 +125,39 @@ void emit_decode(const char* codec, double t, size_t reads, const Check& c, int 
                 c.bad == 0 && c.got == kFrames * (reps + 1) ? "true" : "false");
 }
 
+// T threads, each: make(tid) -> a feed function (created on that thread, so a
+// handler's resident slot belongs to it); one untimed warm-up pass, then
+// `passes` passes of the wire in 64 KiB reads.  Returns wall seconds from the
+// common start to the last thread's end.
+double time_threads(int T, int passes, const std::vector<uint8_t>& wire,
+                    const std::function<std::function<void(uint8_t*, size_t)>(int)>& make)
+{
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::function<void(uint8_t*, size_t)> feed = make(t);
+            std::vector<uint8_t> buf(kRead);
+            auto pass = [&] {
+                for (size_t i = 0; i < wire.size(); i += kRead) {
+                    const size_t n = std::min(kRead, wire.size() - i);
+                    std::memcpy(buf.data(), wire.data() + i, n);  // recv
+                    feed(buf.data(), n);
+                }
+            };
+            pass();
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            for (int p = 0; p < passes; ++p) pass();
+        });
+    while (ready.load() < T) std::this_thread::yield();
+    const auto t0 = Clock::now();
+    go.store(true, std::memory_order_release);
+    for (auto& x : th) x.join();
+    return secs(Clock::now() - t0);
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -175,6 +219,55 @@ int main(int argc, char** argv)
         ok &= c.bad == 0 && c.got == kFrames * (reps + 1) && (resident ? jobs1 > jobs0 : jobs1 == jobs0);
     }
     kmws_resident_enable(0, 1);
+
+    // the decode on T loop threads at once
+    const int passes = std::max(2, reps);
+    for (const char* codec : {"kuma_oracle", "kmws_resident", "kmws_launch"}) {
+        for (int T : {1, 2, 4, 8}) {
+            std::vector<Check> checks(T, Check{&plain});
+            std::vector<std::unique_ptr<kmws::ws::WSHandler>> hs(T);
+            std::vector<orc_decoder*> ods(T, nullptr);
+            const std::string c = codec;
+            uint64_t jobs0 = 0, jobs1 = 0;
+            kmws_resident_info(0, &jobs0, nullptr, nullptr);
+            const double t = time_threads(T, passes, wire, [&](int tid) -> std::function<void(uint8_t*, size_t)> {
+                Check* ck = &checks[tid];
+                if (c == "kuma_oracle") {
+                    ods[tid] = orc_decoder_create(1);
+                    orc_decoder* d = ods[tid];
+                    return [d, ck](uint8_t* p, size_t n) { orc_decoder_feed(d, p, n, orc_cb, ck); };
+                }
+                kmws_resident_enable(0, c == "kmws_resident" ? 1 : 0);  // this thread's calls
+                hs[tid].reset(new kmws::ws::WSHandler());
+                kmws::ws::WSHandler* h = hs[tid].get();
+                h->setMode(kmws::ws::WSMode::SERVER);
+                h->setFrameCallback([ck](kmws::ws::FrameHeader, kmws::ws::BufferChain& b) {
+                    ck->frame(static_cast<const uint8_t*>(b.readPtr()), b.length());
+                    return 0;
+                });
+                return [h](uint8_t* p, size_t n) {
+                    const kmws::ws::WSError e = h->handleData(p, n);
+                    if (e != kmws::ws::WSError::NOERR && e != kmws::ws::WSError::NEED_MORE_DATA) std::exit(4);
+                };
+            });
+            kmws_resident_info(0, &jobs1, nullptr, nullptr);
+            bool exact = true;
+            for (const Check& ck : checks) exact &= ck.bad == 0 && ck.got == kFrames * (passes + 1);
+            for (orc_decoder* d : ods)
+                if (d) orc_decoder_destroy(d);
+            hs.clear();
+            const bool resident = c == "kmws_resident";
+            exact &= c == "kuma_oracle" || (resident ? jobs1 > jobs0 : jobs1 == jobs0);
+            ok &= exact;
+            const double bytes = (double)kFrames * kLen * passes * T;
+            std::printf("{\"case\": \"decode_sync_threads\", \"codec\": \"%s\", \"threads\": %d, \"passes\": %d, "
+                        "\"frames_per_pass\": %d, \"read_bytes\": %zu, \"GiB_s\": %.3f, \"us_per_read_per_thread\": %.3f, "
+                        "\"resident_jobs\": %llu, \"verified\": %s}\n",
+                        codec, T, passes, kFrames, kRead, bytes / t / (1u << 30),
+                        t / ((double)reads * passes) * 1e6, (unsigned long long)(jobs1 - jobs0), exact ? "true" : "false");
+            std::fflush(stdout);
+        }
+    }
 
     // handleDataMask per send
     for (size_t len : {(size_t)1024, (size_t)4096, (size_t)65536}) {

@@ -468,14 +468,14 @@ def test_pack_headers_lookback_timeout_sets_its_own_bit(T):
     """VERDICT r03 #7 / ADVICE r03: a look-back predecessor that never
     publishes must end the wait with kStatusLookbackTimeout (4), not the
     bad-descriptor bit, and the call must return.  Test-only library
-    (kuma_amd/build.py LOOKBACK_TEST_DEFINES): tile 1 of the header pack never
+    (kuma_amd/build.py TEST_DEFINES): tile 1 of the header pack never
     publishes, the spin bound is 4096 polls.  The product binding then refuses
     the offsets (KmwsError with the workspace status)."""
     import ctypes as C
     from kuma_amd import build as kb
     from kuma_amd import kmws
-    assert os.path.exists(kb.LOOKBACK_TEST_LIB), "run __graft_entry__.build()"
-    L = C.CDLL(kb.LOOKBACK_TEST_LIB)
+    assert os.path.exists(kb.TEST_LIB), "run __graft_entry__.build()"
+    L = C.CDLL(kb.TEST_LIB)
     vp = C.c_void_p
     L.kmws_pack_headers.restype, L.kmws_pack_headers.argtypes = C.c_int, [vp, vp, C.c_uint32, vp, vp, vp, vp,
                                                                          C.c_size_t, vp]
@@ -502,8 +502,62 @@ def test_pack_headers_lookback_timeout_sets_its_own_bit(T):
     # a nonzero status after the call surfaces as an error in the binding
     ws.status = lambda stream=None: 4
     with pytest.raises(kmws.KmwsError) as e:
-        kmws.pack_headers(descs, fl, hdr, None, woff, ws)
+        kmws.pack_headers(descs, fl, hdr, None, woff, ws, check=True)
     assert e.value.ws_status == 4
+
+
+def test_chunk_scan_lookback_timeout_stores_nothing(T):
+    """the chunk form's one-pass front (chunk_scan_kernel, used when
+    dst_cap / n < 16 KiB) waits on a decoupled look-back too.  In the test build
+    tile 1 never publishes: encode_batch and gather_unmask then report status
+    bit 4 (not the bad-input bit), store nothing into dst, and the binding's
+    check=True raises; the product library on the same batch is exact."""
+    import ctypes as C
+    from kuma_amd import build as kb
+    from kuma_amd import kmws
+    assert os.path.exists(kb.TEST_LIB), "run __graft_entry__.build()"
+    TL = kmws.bind(C.CDLL(kb.TEST_LIB))
+    n = 3 * 2048 + 7
+    rng = np.random.default_rng(45)
+    lens = rng.integers(1, 120, size=n)
+    keys = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.int64)
+    offs = np.arange(n, dtype=np.int64) * 128
+    src = T.from_numpy(rng.integers(0, 256, size=n * 128, dtype=np.uint8)).cuda()
+    descs = kmws.make_descs(offs, lens, keys)
+    fl = T.full((n,), 0x182, dtype=T.int16, device="cuda")
+    h = kmws._stream_handle()
+    for what in ("encode", "gather"):
+        cap = int(lens.sum()) + (6 * n if what == "encode" else 0)
+        assert cap // n < 16384  # the chunk form
+        dst = T.full((cap,), 0xAB, dtype=T.uint8, device="cuda")
+        off = T.zeros(n + 1, dtype=T.int64, device="cuda")
+        ws = kmws.Workspace(kmws.copy_workspace_size(n, cap))
+        if what == "encode":
+            rc = TL.kmws_encode_batch(src.data_ptr(), descs.data_ptr(), fl.data_ptr(), n, dst.data_ptr(), cap,
+                                      off.data_ptr(), ws.ptr, ws.nbytes, h)
+        else:
+            rc = TL.kmws_gather_unmask(src.data_ptr(), descs.data_ptr(), n, dst.data_ptr(), cap, off.data_ptr(),
+                                       ws.ptr, ws.nbytes, h)
+        assert rc == 0
+        st = C.c_uint32(0)
+        assert TL.kmws_read_status(ws.ptr, C.byref(st), h) == 0
+        assert st.value & 4 and not st.value & 1, (what, st.value)
+        assert int((dst != 0xAB).sum()) == 0, what  # nothing stored
+        # the product library: clean status, the binding's check passes
+        if what == "encode":
+            kmws.encode_batch(src, descs, fl, dst, off, ws, check=True)
+            hl = 6
+        else:
+            kmws.gather_unmask(src, descs, dst, off, ws, check=True)
+            hl = 0
+        assert np.array_equal(off.cpu().numpy(), np.concatenate([[0], np.cumsum(lens + hl)]))
+        ws.status = lambda stream=None: 4  # a nonzero status surfaces as an error with check=True
+        with pytest.raises(kmws.KmwsError) as e:
+            if what == "encode":
+                kmws.encode_batch(src, descs, fl, dst, off, ws, check=True)
+            else:
+                kmws.gather_unmask(src, descs, dst, off, ws, check=True)
+        assert e.value.ws_status == 4
 
 
 def test_find_headers_streams_matches_host_walk(T):

@@ -73,8 +73,8 @@ def sync(reps: int):
            "note": "in-process C++ driver, one codec call per 64 KiB read (decode) / per send (mask); "
                    "kuma_oracle = the oracle's restatement of kuma's codec on one core"}
     for x in rows:
-        out.setdefault(x["case"], {}).setdefault(str(x.get("len", "cfg1")), {})[x["codec"]] = \
-            x.get("GiB_s") if x["case"] == "decode_sync" else x.get("us_per_call")
+        out.setdefault(x["case"], {}).setdefault(str(x.get("len", x.get("threads", "cfg1"))), {})[x["codec"]] = \
+            x.get("GiB_s") if x["case"].startswith("decode_sync") else x.get("us_per_call")
     return out
 
 
