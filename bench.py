@@ -168,24 +168,32 @@ def schedule_name(schedule: int) -> str:
     return kind + ", automatic store policy (temporal on tile-aligned batches)"
 
 
-def traffic_from_profile(frames: int, frame_len: int, kernel: str, schedule=None):
+def traffic_from_profile(frames: int, frame_len: int, kernel: str, schedule=None, profiles_dir=None):
     """HBM bytes per launch of the unmask kernel from the committed PMC passes
     (profiles/*traffic*.json, written by tools/pmc_traffic.py) measured on this
-    exact configuration: the latest one for this schedule if there is one, else
-    the latest for the kernel; None if there is none."""
+    exact configuration: the newest one (by the `measured_at` time each record
+    carries) for this schedule if there is one, else the newest for the
+    kernel; None if there is none."""
+    import datetime
     import glob
-    same, any_ = None, None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
+
+    def when(t):
+        try:
+            return datetime.datetime.fromisoformat(t.get("measured_at", "")).timestamp()
+        except ValueError:
+            return float("-inf")
+    same, any_ = [], []
+    for path in glob.glob(os.path.join(profiles_dir or os.path.join(ROOT, "profiles"), "*traffic*.json")):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
         if t.get("frames") == frames and t.get("frame_len") == frame_len and t.get("kernel") == kernel:
-            any_ = t
+            any_.append(t)
             if schedule is not None and t.get("schedule") == schedule:
-                same = t
-    best = same or any_
-    return None if best is None else best.get("hbm_bytes_per_launch")
+                same.append(t)
+    pool = same or any_
+    return max(pool, key=when).get("hbm_bytes_per_launch") if pool else None
 
 
 def cpu_baseline_cfg1(run) -> float:

@@ -67,6 +67,26 @@
 
 namespace kmws {
 
+// kuma's FrameHeader (wsdefs.h:74-88: bitfields fin..plen, xpl, maskey,
+// length) -- or any type with those fields -- as the C ABI's kmws_frame_hdr.
+template <class FrameHeader>
+inline kmws_frame_hdr to_c_header(const FrameHeader& hdr)
+{
+    kmws_frame_hdr k;
+    std::memset(&k, 0, sizeof(k));
+    k.fin = hdr.fin;
+    k.rsv1 = hdr.rsv1;
+    k.rsv2 = hdr.rsv2;
+    k.rsv3 = hdr.rsv3;
+    k.opcode = hdr.opcode;
+    k.mask = hdr.mask;
+    k.plen = hdr.plen;
+    k.length = hdr.length;
+    std::memcpy(k.maskey, hdr.maskey, KMWS_MASK_KEY_SIZE);
+    return k;
+}
+inline kmws_frame_hdr to_c_header(const kmws_frame_hdr& hdr) { return hdr; }
+
 // The deferred receive batch of one event-loop thread, shared by every handler
 // on that loop, and the once-per-iteration hook that runs it.
 class RxLoop {
@@ -249,11 +269,27 @@ public:
     // plen, header packed now; masked with hdr.maskey when hdr.mask is set and
     // plen > 0 (kuma's client mode, :384-388).  Returns the header length
     // (2..14) or a negative kmws_status.
-    int send(Conn* c, const kmws_frame_hdr& hdr, const uint8_t* payload, size_t plen)
+    // (hdr: kuma's FrameHeader or a kmws_frame_hdr)
+    template <class FrameHeader>
+    int send(Conn* c, const FrameHeader& hdr, const uint8_t* payload, size_t plen)
     {
         const uint8_t* segs[1] = {payload};
         const size_t lens[1] = {plen};
-        return sendChain(c, hdr, segs, lens, plen ? 1 : 0);
+        return sendChain(c, to_c_header(hdr), segs, lens, plen ? 1 : 0);
+    }
+
+    // sendWsFrame(hdr, const KMBuffer&) (:405-436) over kuma's chain
+    // (KMBuffer::begin/end, readPtr, length: kmbuffer.h:706-772).
+    template <class FrameHeader, class Buffer>
+    int sendBuffer(Conn* c, const FrameHeader& hdr, const Buffer& buf)
+    {
+        std::vector<const uint8_t*> segs;
+        std::vector<size_t> lens;
+        for (auto it = buf.begin(); it != buf.end(); ++it) {
+            segs.push_back(static_cast<const uint8_t*>(it->readPtr()));
+            lens.push_back(it->length());
+        }
+        return sendChain(c, to_c_header(hdr), segs.data(), lens.data(), segs.size());
     }
 
     // sendWsFrame(hdr, KMBuffer) (:405-436): the chain's segments, the key
@@ -538,17 +574,7 @@ public:
     // WSHandler::encodeFrameHeader (WSHandler.cpp:46-106): 2/4/10 (+4) bytes
     static int encodeFrameHeader(FrameHeader hdr, uint8_t hdr_buf[KMWS_MAX_HEADER_SIZE])
     {
-        kmws_frame_hdr k;
-        std::memset(&k, 0, sizeof(k));
-        k.fin = hdr.fin;
-        k.rsv1 = hdr.rsv1;
-        k.rsv2 = hdr.rsv2;
-        k.rsv3 = hdr.rsv3;
-        k.opcode = hdr.opcode;
-        k.mask = hdr.mask;
-        k.plen = hdr.plen;
-        k.length = hdr.length;
-        std::memcpy(k.maskey, hdr.maskey, KMWS_MASK_KEY_SIZE);
+        const kmws_frame_hdr k = to_c_header(hdr);
         return kmws_encode_header(&k, hdr_buf);
     }
 

@@ -30,9 +30,9 @@ TEST_DEFINES = ("KMWS_TEST_SKIP_PUBLISH_TILE=1", "KMWS_LOOKBACK_SPIN_LIMIT=4096"
 RESIDENT_STALL_KEY = 0xDEAD5E00
 
 
-def sources():
-    return sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) +
-                  glob.glob(os.path.join(HERE, "csrc", "*.cpp")))
+def sources(srcdir: str | None = None):
+    d = srcdir or os.path.join(HERE, "csrc")
+    return sorted(glob.glob(os.path.join(d, "*.hip")) + glob.glob(os.path.join(d, "*.cpp")))
 
 
 def deps():
@@ -47,17 +47,19 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in deps())
 
 
-def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
-    """Compiles the library; `out` + `defines` (-D flags) make a tuning variant
-    (tools/ab_pack.py) without touching the product library."""
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=(),
+          srcdir: str | None = None) -> str:
+    """Compiles the library; `out` + `defines` (-D flags) make the test build,
+    `out` + `srcdir` (a patched copy of csrc/, tools/build_variant.py) a tuning
+    variant, without touching the product library."""
     if out is None and not force and up_to_date():
         return LIB
     lib = out or LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     objs = []
-    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", srcdir or os.path.join(HERE, "csrc")]
     cmds = []
-    for src in sources():
+    for src in sources(srcdir):
         obj = os.path.join(LIB_DIR, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
         cmds.append(["hipcc", "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                      "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *inc, "-c", src, "-o", obj])

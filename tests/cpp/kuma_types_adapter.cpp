@@ -191,6 +191,32 @@ int main()
         h.setRxLoop(&loop);
         CHECK(loop.valid() == (kmws_device_count() > 0) && (h.rxLoop() != nullptr) == loop.valid());
     }
+    // the send side, as WebSocket::Impl::sendWsFrame would call it (INTEGRATION.md
+    // sec.3.3) with kuma's FrameHeader and a two-segment KMBuffer chain; without
+    // a device the TxLoop is invalid and refuses the send
+    {
+        std::vector<kmws::TxLoop::Task> tasks;
+        kmws::TxLoop tx([&tasks](kmws::TxLoop::Task t) { tasks.push_back(std::move(t)); });
+        std::string wrote;
+        kmws::TxLoop::Conn* conn = tx.open([&wrote](const iovec* v, int n) {
+            for (int i = 0; i < n; ++i) wrote.append(static_cast<const char*>(v[i].iov_base), v[i].iov_len);
+            return 0;
+        });
+        FrameHeader hdr;
+        std::memset(static_cast<void*>(&hdr), 0, sizeof(hdr));
+        hdr.fin = 1;
+        hdr.opcode = (uint8_t)WSOpcode::TEXT;
+        char a[] = "Hel", b[] = "lo";
+        KMBuffer b1(a, 3, 3), b2(b, 2, 2);
+        b1.append(&b2);
+        const int r = tx.sendBuffer(conn, hdr, b1);  // unmasked (server mode): written at once
+        if (kmws_device_count() == 0) {
+            CHECK(!tx.valid() && r == KMWS_ERR_INVALID_STATE && wrote.empty());
+        } else {
+            CHECK(r == 2 && wrote == std::string("\x81\x05Hello", 7));
+            (void)tx.close(conn);
+        }
+    }
     if (g_fail) {
         std::printf("%d checks failed\n", g_fail);
         return 1;

@@ -152,3 +152,26 @@ def test_cpu_baseline_cores_are_the_effective_count(monkeypatch):
     cb = bench.cpu_baseline(0.2, bench.effective_cores(), 4096, 1)
     assert cb["cores"] == 2 and cb["affinity_cores"] == 256 and cb["cgroup_cpu_quota_cores"] == 2.0
     assert cb["value"] > 0 and cb["single_core_GiB_s"] > 0 and "not calibrated" in cb["sample"]
+
+
+def test_traffic_from_profile_takes_the_newest_record(tmp_path):
+    """`traffic` is the newest PMC record for the bench's
+    schedule by the time stamped in it, not the last file name in sort order;
+    records without a stamp rank below stamped ones; another schedule's
+    record is used only when none matches."""
+    import json
+    import bench
+    def rec(name, when, val, sched=536870914):
+        t = {"kernel": bench.UNMASK_KERNEL, "frames": 8, "frame_len": 64, "schedule": sched,
+             "hbm_bytes_per_launch": val}
+        if when:
+            t["measured_at"] = when
+        (tmp_path / name).write_text(json.dumps(t))
+    rec("r09_pmc_traffic.json", "2026-10-17T03:00:00+00:00", 1.0)
+    rec("r05b_pmc_traffic.json", "2026-10-18T09:00:00+00:00", 2.0)
+    rec("r07_pmc_traffic.json", None, 3.0)
+    rec("r08_pmc_traffic.json", "2026-10-19T09:00:00+00:00", 4.0, sched=5)
+    f = bench.traffic_from_profile
+    assert f(8, 64, bench.UNMASK_KERNEL, 536870914, profiles_dir=str(tmp_path)) == 2.0
+    assert f(8, 64, bench.UNMASK_KERNEL, 7, profiles_dir=str(tmp_path)) == 4.0  # no match: newest of any
+    assert f(8, 65, bench.UNMASK_KERNEL, 7, profiles_dir=str(tmp_path)) is None

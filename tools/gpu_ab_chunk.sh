@@ -3,9 +3,10 @@
 # timed, RUN_TAG=<tag>:
 #  1. the pack / configs / fuzz GPU tests on the product build;
 #  2. tools/ab_pack.py (cfg4, cfg3, small frames) per build, each loaded alone:
-#     product (chunk form below a 16 KiB mean region, unit form above),
-#     tools/ab/libkmws_chunks.so (chunk form always, KMWS_PACK_UNITS=2),
-#     _units.so (unit form always, KMWS_PACK_UNITS=1);
+#     the product (chunk form below a 16 KiB mean region, unit form above) and
+#     any other build named in LIBS -- the product sources carry no tuning
+#     switches (round 5): a variant is built from a patched copy of
+#     kuma_amd/csrc (tools/build_variant.py <patch> <out.so>);
 #  3. FETCH_SIZE and WRITE_SIZE passes (separate runs) of the product on cfg4.
 # LIBS="name:path ..." / CFGS / QUICK=1 (step 2 only) select another A/B.
 set -o pipefail
@@ -14,7 +15,7 @@ TAG=${RUN_TAG:?set RUN_TAG}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-LIBS=${LIBS:-"product:kuma_amd/lib/libkmws_gpu.so chunks:tools/ab/libkmws_chunks.so units:tools/ab/libkmws_units.so"}
+LIBS=${LIBS:-"product:kuma_amd/lib/libkmws_gpu.so"}
 CFGS=${CFGS:-cfg4,cfg3,small}
 if [ -z "$QUICK" ]; then
   timeout -k 10 500 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread \

@@ -7,6 +7,7 @@ stores; both are in KiB.
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <kernel-substr> <frames> <frame_len> <out.json>
 """
 import csv
+import datetime
 import glob
 import json
 import os
@@ -51,7 +52,8 @@ def main():
            "read_bytes_corrected": read_bytes, "write_bytes": write_bytes,
            "hbm_bytes_per_launch": read_bytes + write_bytes, "algorithmic_bytes_per_launch": alg,
            "traffic_over_algorithmic": (read_bytes + write_bytes) / alg,
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB->bytes x1024"}
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB->bytes x1024",
+           "measured_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")}
     if schedule is not None:
         res["schedule"] = schedule
     json.dump(res, open(out, "w"), indent=1)
