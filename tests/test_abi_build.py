@@ -202,3 +202,36 @@ def test_rx_flush_bench_every_mode_exact(tmp_path):
     assert [x["mode"] for x in rows] == ["flush", "submitpoll", "noresident", "flush", "submitpoll"]
     assert all(x["bad"] == 0 and x["delivered"] == 250 * 4 for x in rows)
     assert rows[0]["resident_jobs"] >= 250 and rows[2]["resident_jobs"] == rows[1]["resident_jobs"]
+
+
+def _build_txloop(tmp_path):
+    """tests/cpp/txloop_check.cpp: kmws::TxLoop against kuma's send path restated in oracle/."""
+    lib = kb.build()
+    from oracle import oracle as orc
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    exe = tmp_path / "txloop_check"
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "txloop_check.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", str(exe)])
+    return exe
+
+
+def test_txloop_program_builds(tmp_path):
+    assert _build_txloop(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_txloop_matches_kuma_send_path(tmp_path):
+    """kmws::TxLoop (sendWsFrame's batched replacement) over three
+    connections of one loop, masked and unmasked frames, chains, empty payloads,
+    payloads larger than its pinned ring, a ring that wraps: every connection's
+    bytes equal kuma's frames (oracle) in send order; callers' buffers untouched."""
+    import json
+    exe = _build_txloop(tmp_path)
+    for seed in ("1", "2", "3"):
+        r = subprocess.run([str(exe), seed, "3000"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["exact"] and d["callers_buffers_changed"] == 0 and d["larger_than_ring"] > 0
