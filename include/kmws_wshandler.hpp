@@ -179,9 +179,10 @@ private:
 // payload queued in the iteration with ONE GPU job and writes each
 // connection's frames, in send order, as soon as their generation's mask has
 // completed -- the GPU round trip overlaps the next iteration instead of
-// stalling every send.  At most `max_inflight` generations are in flight (2:
-// the loop fills and submits iteration k while iteration k - 1's masks run);
-// a third waits for the oldest.
+// stalling every send.  At most `max_inflight` generations are in flight
+// after a run (1: the task submits iteration k, then writes iteration k - 1,
+// whose masks ran while the loop filled k -- waiting for them only if they
+// have not finished yet).
 //
 // Differences from sendWsFrame, observable only to the sender:
 //  * the frame reaches the socket at the iteration's task, not before send()
@@ -212,7 +213,7 @@ public:
         int last_ = 0;
     };
 
-    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)16 << 20, int max_inflight = 2)
+    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)16 << 20, int max_inflight = 1)
         : post_(std::move(post)), batch_(kmws_tx_batch_create(device)), max_inflight_(max_inflight < 1 ? 1 : max_inflight),
           alive_(std::make_shared<bool>(true))
     {

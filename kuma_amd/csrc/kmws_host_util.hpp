@@ -287,8 +287,9 @@ private:
             if (st != KMWS_OK) return st;
         }
         if (hipEventRecord(done_, stream_) != hipSuccess) return KMWS_ERR_FAILED;
-        // ~16 GB/s over PCIe: 64 KiB ~ 4 us on top of a launch's ~50 us
-        spin_us_ = std::min<uint64_t>(2000, 50 + (bytes >> 14));
+        // spin for about twice what the job should take (a launch's ~20 us, then
+        // the payload over PCIe at ~8 GB/s each way), at most 2 ms
+        spin_us_ = std::min<uint64_t>(2000, 2 * (20 + (bytes >> 13)));
         launched_ = true;
         return KMWS_OK;
     }
@@ -346,7 +347,7 @@ private:
     uint64_t saved_span_ = 0;
     uint8_t* saved_dv_ = nullptr;
     std::vector<kmws_desc> saved_extra_;
-    uint64_t spin_us_ = 50;
+    uint64_t spin_us_ = 40;
     uint8_t* h_ = nullptr;
     uint8_t* dv_h_ = nullptr;
     size_t cap_ = 0, len_ = 0;

@@ -346,6 +346,12 @@ T ld_acq(const T* p)
     return __atomic_load_n(p, __ATOMIC_ACQUIRE);
 }
 
+// Is job s of a slot finished, given the slot's done word?  Jobs of a slot run
+// one at a time in number order (40-bit, wrapping), so a done word at or past
+// s means s has run -- a ticket may be waited for after a later job of the
+// same slot finished.
+inline bool job_done(uint64_t done, uint64_t s) { return ((done - s) & kJobMask) < (1ull << 39); }
+
 using Clock = std::chrono::steady_clock;
 
 // One per device, shared by every host thread.  Slots are claimed with one
@@ -451,10 +457,10 @@ public:
     int test(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
-        if (ld_acq(&sl.done) == s) return 1;
+        if (job_done(ld_acq(&sl.done), s)) return 1;
         const uint64_t cur = ld_acq(&inc_);
         if (ld_acq(&mb_->exited) == cur) {
-            if (ld_acq(&sl.done) == s) return 1;
+            if (job_done(ld_acq(&sl.done), s)) return 1;
             if (relaunch(cur) == 0 && withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
         }
         return 0;
@@ -470,19 +476,19 @@ public:
         const auto t0 = Clock::now();
         Clock::time_point orphan{};
         for (uint32_t spin = 0;; ++spin) {
-            if (ld_acq(&sl.done) == s) return KMWS_OK;
+            if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
             cpu_relax();
             if ((spin & 255) != 255) continue;
             const uint64_t cur = ld_acq(&inc_);
             if (ld_acq(&mb_->exited) == cur) {  // the whole grid left: relaunch (the new one takes job s)
-                if (ld_acq(&sl.done) == s) return KMWS_OK;
+                if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
                 if (relaunch(cur) == 0) {
                     if (withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
                     continue;
                 }
                 orphan = Clock::time_point{};
             } else if (ld_acq(&sl.gone) == cur) {  // this slot's workgroup left, others run on
-                if (ld_acq(&sl.done) == s) return KMWS_OK;
+                if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
                 const auto now = Clock::now();
                 if (orphan == Clock::time_point{}) orphan = now;
                 else if (now - orphan > std::chrono::microseconds(kResOrphanUs) && withdraw(b, s, cur))
@@ -515,7 +521,8 @@ private:
     {
         ResSlot& sl = mb_->slot[b];
         std::lock_guard<std::mutex> lk(launch_mu_);
-        if (ld_acq(&inc_) != cur || ld_acq(&sl.done) == s) return false;
+        // (a later job was posted on the slot only after s was done)
+        if (ld_acq(&inc_) != cur || seq_[b] != s || job_done(ld_acq(&sl.done), s)) return false;
         if (ld_acq(&sl.gone) != cur && ld_acq(&mb_->exited) != cur) return false;
         const uint64_t prev = (s - 1) & kJobMask;
         seq_[b] = prev;
@@ -534,7 +541,7 @@ private:
         __atomic_fetch_or(&sl.word, kQuitBit, __ATOMIC_RELEASE);
         const auto t0 = Clock::now();
         for (uint32_t spin = 0;; ++spin) {
-            if (ld_acq(&sl.done) == s) {
+            if (job_done(ld_acq(&sl.done), s)) {
                 std::lock_guard<std::mutex> lk(launch_mu_);
                 __atomic_fetch_and(&sl.word, ~kQuitBit, __ATOMIC_RELEASE);
                 return KMWS_OK;

@@ -212,7 +212,7 @@ def _check_descs(descs) -> int:
 
 def _check(st: int, what: str) -> None:
     if st != OK:
-        raise RuntimeError(f"{what} failed with kmws_status {st}")
+        raise KmwsError(st, what)
 
 
 # ====================== host codec (WSHandler mirror) ======================

@@ -26,14 +26,16 @@
 //        the client sends through its loop thread's kmws::TxLoop (sendWsFrame's
 //        replacement: header packed and payload copied into the pinned send
 //        ring at send, one mask job per iteration, frames written by the posted
-//        task once their generation completed, two generations in flight).
+//        task once their generation completed, one generation in flight after
+//        each task).
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [noresident]
-// (noresident: both loop threads switch their resident worker off -- every GPU
-// job a launch and a wait, the A/B of kmws_resident.hip; submitpoll: the gpu
-// mode's flushes replaced by submit + poll(wait))
+// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [variant]
+// (variant noresident: both loop threads switch their resident worker off --
+// every GPU job a launch and a wait, the A/B of kmws_resident.hip; submitpoll:
+// the gpu mode's flushes replaced by submit + poll(wait); inflight2: the
+// adapter's TxLoop keeps two generations in flight instead of one)
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -161,6 +163,7 @@ struct LoopObjs {
 bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
 bool g_noresident = false;
 bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flushes
+int g_inflight = 1;         // adapter mode: the TxLoop's generations in flight after a run (inflight2: 2)
 
 double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
@@ -431,6 +434,7 @@ int main(int argc, char** argv)
     if (argc > 4) kFlushBytes = (size_t)std::atoll(argv[4]);
     g_noresident = argc > 5 && std::string(argv[5]) == "noresident";
     g_submitpoll = argc > 5 && std::string(argv[5]) == "submitpoll";
+    if (argc > 5 && std::string(argv[5]) == "inflight2") g_inflight = 2;
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     const bool adapter = mode == "adapter";
     g_sync = mode == "sync";
@@ -455,7 +459,7 @@ int main(int argc, char** argv)
         if (adapter) {
             lo.rxloop = new kmws::RxLoop(nullptr, 0);
             if (!lo.rxloop->valid() || lo.rxloop->attachRing(lo.rring, kRing) != KMWS_OK) return 3;
-            lo.txloop = new kmws::TxLoop(nullptr, 0);
+            lo.txloop = new kmws::TxLoop(nullptr, 0, (size_t)16 << 20, g_inflight);
             if (!lo.txloop->valid()) return 3;
         } else if (kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK) {
             return 3;

@@ -507,6 +507,42 @@ def test_resident_more_threads_than_slots_launch_instead():
     assert kmws.resident_info()["slots_claimed"] == base
 
 
+def test_resident_and_launch_paths_interleaved_on_many_threads():
+    """Four threads at once, 40 jobs each of 1 B to 512 KiB at odd offsets,
+    chains of up to three segments: jobs of up to 64 KiB run on each thread's
+    slot of the resident grid, larger ones are launched on the thread's own
+    stream, interleaved on every thread.  Every byte equals the oracle's, and
+    exactly the jobs that fit the worker ran on it."""
+    import threading
+    res = {}
+
+    def run(tid):
+        rng = random.Random(1000 + tid)
+        bad = small = 0
+        for i in range(40):
+            n = rng.choice([rng.randrange(1, 4096), rng.randrange(32768, 70000), rng.randrange(70000, 524288)])
+            key = bytes(rng.randrange(256) for _ in range(4))
+            data = rng.randbytes(n + 17)
+            off = rng.randrange(0, 17)
+            cuts = sorted(rng.randrange(0, n + 1) for _ in range(rng.randrange(0, 3)))
+            segs = [bytearray(data[off + a:off + b]) for a, b in zip([0] + cuts, cuts + [n])]
+            want = orc.mask_bytes(key, data[off:off + n])
+            kmws.handle_data_mask(key, segs)
+            bad += b"".join(segs) != want
+            small += n <= 65536
+        res[tid] = (bad, small)
+
+    before = kmws.resident_info()
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    after = kmws.resident_info()
+    assert all(b == 0 for b, _ in res.values()), res
+    assert after["jobs"] - before["jobs"] == sum(s for _, s in res.values()), (before, after, res)
+
+
 def _testhooks_lib():
     """The test-only build (kuma_amd/build.py TEST_DEFINES): job timeout 50 ms,
     drain 150 ms, a job keyed 0xDEAD5Exx stalls its workgroup xx * 10 ms."""
