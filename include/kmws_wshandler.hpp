@@ -213,7 +213,10 @@ public:
         int last_ = 0;
     };
 
-    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)16 << 20, int max_inflight = 1)
+    // ring_bytes: the pinned send ring (a small one stays in the CPU's caches:
+    // the payload copies and the socket writes hit it); a payload that does
+    // not fit goes through a buffer of its own
+    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)1 << 20, int max_inflight = 1)
         : post_(std::move(post)), batch_(kmws_tx_batch_create(device)), max_inflight_(max_inflight < 1 ? 1 : max_inflight),
           alive_(std::make_shared<bool>(true))
     {

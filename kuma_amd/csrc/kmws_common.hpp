@@ -106,6 +106,9 @@ constexpr int kResMaxDescs = 128;
 // profiles/r04w_rx_flush_bench.jsonl), below it faster (10.7 vs 18.5 us at 16
 // KiB); above it the launch's several blocks move the bytes faster.
 constexpr uint64_t kResMaxBytes = 64u << 10;
+// An asynchronous job (an rx / tx batch's submit) costs the loop thread no
+// launch however long it runs; up to this size it goes to the worker too.
+constexpr uint64_t kResMaxBytesAsync = 256u << 10;
 struct ResidentJob {
     int device = -1;
     int slot = -1;
@@ -118,7 +121,8 @@ struct ResidentJob {
 // the worker off, its slot still runs a job, or the worker is unusable -- the
 // caller launches instead.
 kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
-                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job);
+                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job,
+                          uint64_t max_bytes = kResMaxBytes);
 // 1: done; 0: running; KMWS_ERR_NOT_SUPPORTED: withdrawn, never run (launch it).
 int resident_test(const ResidentJob& job);
 // KMWS_OK: done.  KMWS_ERR_NOT_SUPPORTED: withdrawn, never run (launch it).

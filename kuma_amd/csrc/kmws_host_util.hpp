@@ -132,7 +132,7 @@ public:
     kmws_status run(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
                     const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
     {
-        kmws_status st = launch(extra_base, extra_span, extra, extra_dv);
+        kmws_status st = launch(extra_base, extra_span, extra, extra_dv, kResMaxBytes);
         if (st != KMWS_OK) return st;
         return wait();
     }
@@ -188,13 +188,16 @@ public:
     }
 
     // Enqueue the unmask of every staged descriptor (and `extra`) without
-    // waiting: a job of at most kResMaxDescs payloads and kResMaxBytes bytes is
+    // waiting: a job of at most kResMaxDescs payloads and max_res_bytes bytes is
     // posted on the calling thread's slot of the device's resident worker (no
     // launch; kmws_resident.hip), anything else is launched on the stage's
     // stream (launch_unmask_pieces: no plan kernels, no copies, no status
     // read-back) with its completion event recorded.
+    // max_res_bytes: the largest job posted on the worker (a synchronous run()
+    // keeps kResMaxBytes: one workgroup is slower than a launch's many above it).
     kmws_status launch(uint8_t* extra_base = nullptr, uint64_t extra_span = 0,
-                       const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr)
+                       const std::vector<kmws_desc>* extra = nullptr, uint8_t* extra_dv = nullptr,
+                       uint64_t max_res_bytes = kResMaxBytesAsync)
     {
         const size_t n1 = descs_.size(), n2 = extra ? extra->size() : 0;
         if (n1 + n2 == 0) return KMWS_OK;
@@ -206,7 +209,7 @@ public:
         if (n1 && !dv_h_) return KMWS_ERR_FAILED;
         if (n1 + n2 <= (size_t)kResMaxDescs) {
             const kmws_status st = resident_post(device_, descs_.data(), dv_h_, n1, n2 ? extra->data() : nullptr,
-                                                 extra_dv, n2, &res_);
+                                                 extra_dv, n2, &res_, max_res_bytes);
             if (st == KMWS_OK) {  // kept for a launch if the worker withdraws the job
                 saved_base_ = extra_base;
                 saved_span_ = extra_span;
@@ -288,8 +291,12 @@ private:
         }
         if (hipEventRecord(done_, stream_) != hipSuccess) return KMWS_ERR_FAILED;
         // spin for about twice what the job should take (a launch's ~20 us, then
-        // the payload over PCIe at ~8 GB/s each way), at most 2 ms
-        spin_us_ = std::min<uint64_t>(2000, 2 * (20 + (bytes >> 13)));
+        // the payload over PCIe at ~8 GB/s each way), at least 1 ms -- a kernel
+        // queued behind the resident grid on a shared hardware queue waits up
+        // to its 1 ms lease, and a parked thread is woken milliseconds late
+        // (loopback rx flushes of 2.6-5.1 ms with a 104 us spin, r05g) -- at
+        // most 2 ms
+        spin_us_ = std::min<uint64_t>(2000, std::max<uint64_t>(1000, 2 * (20 + (bytes >> 13))));
         launched_ = true;
         return KMWS_OK;
     }
@@ -347,7 +354,7 @@ private:
     uint64_t saved_span_ = 0;
     uint8_t* saved_dv_ = nullptr;
     std::vector<kmws_desc> saved_extra_;
-    uint64_t spin_us_ = 40;
+    uint64_t spin_us_ = 1000;
     uint8_t* h_ = nullptr;
     uint8_t* dv_h_ = nullptr;
     size_t cap_ = 0, len_ = 0;

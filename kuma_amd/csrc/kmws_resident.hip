@@ -120,7 +120,7 @@ constexpr int kPollDescs = 31;
 static_assert(kPollDescs < 64, "one lane of wave 0 per polled slot");
 constexpr uint64_t kAddrMask = (1ull << 48) - 1;
 constexpr uint32_t kLenMask = (1u << 21) - 1;  // kResMaxBytes fits
-static_assert(kResMaxBytes <= kLenMask, "tagged length");
+static_assert(kResMaxBytes <= kLenMask && kResMaxBytesAsync <= kLenMask, "tagged length");
 __host__ __device__ __forceinline__ ResDesc tag_desc(ResDesc x, uint64_t job)
 {
     x.addr |= (job & 0xFFFFull) << 48;
@@ -712,7 +712,8 @@ int thread_slot(int device, ResidentWorker** wout)
 // dev_base2 (device views of pinned host memory, offsets relative to them) on
 // the calling thread's slot; see kmws_common.hpp.
 kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev_base, size_t n,
-                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job)
+                          const kmws_desc* descs2, const uint8_t* dev_base2, size_t n2, ResidentJob* job,
+                          uint64_t max_bytes)
 {
     if (n + n2 == 0 || n + n2 > (size_t)kResMaxDescs) return KMWS_ERR_NOT_SUPPORTED;
     ResidentWorker* w = nullptr;
@@ -729,7 +730,7 @@ kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev
         d[k] = ResDesc{(uint64_t)(uintptr_t)(dev_base2 + descs2[i].off), descs2[i].len, descs2[i].key};
         bytes += descs2[i].len;
     }
-    if (bytes > kResMaxBytes) return KMWS_ERR_NOT_SUPPORTED;
+    if (bytes > max_bytes || bytes > kResMaxBytesAsync) return KMWS_ERR_NOT_SUPPORTED;
     uint64_t s = 0;
     const kmws_status st = w->post(b, d, (uint32_t)k, &s);
     if (st != KMWS_OK) return st;

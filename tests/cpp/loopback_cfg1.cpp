@@ -35,7 +35,8 @@
 // (variant noresident: both loop threads switch their resident worker off --
 // every GPU job a launch and a wait, the A/B of kmws_resident.hip; submitpoll:
 // the gpu mode's flushes replaced by submit + poll(wait); inflight2: the
-// adapter's TxLoop keeps two generations in flight instead of one)
+// adapter's TxLoop keeps two generations in flight instead of one; ring16m: its
+// send ring is 16 MiB instead of 1 MiB)
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -98,6 +99,8 @@ double now_s()
 }
 struct Times {  // seconds spent per step in the last connection (breakdown)
     double tx_flush = 0, writev = 0, rx_feed = 0, rx_flush = 0, recv = 0, client = 0;
+    double rx_task_max = 0, rx_wrap = 0;  // adapter: the longest posted rx task; flushes at ring wraps
+    int rx_wraps = 0, rx_inflight_max = 0;
 } g_t;
 
 struct Expect {
@@ -164,6 +167,7 @@ bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
 bool g_noresident = false;
 bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flushes
 int g_inflight = 1;         // adapter mode: the TxLoop's generations in flight after a run (inflight2: 2)
+size_t g_tx_ring = (size_t)1 << 20;  // adapter mode: the TxLoop's pinned send ring (ring16m: 16 MiB)
 
 double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
 {
@@ -271,6 +275,8 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                         const double tf = now_s();
                         if (rx.flush() < 0) std::exit(5);
                         g_t.rx_flush += now_s() - tf;
+                        g_t.rx_wrap += now_s() - tf;
+                        ++g_t.rx_wraps;
                         pos = 0;
                     }
                     double t = now_s();
@@ -291,6 +297,8 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 for (auto& t : now) t();
                 if (rx.lastResult() < 0) std::exit(5);
                 g_t.rx_flush += now_s() - tf;
+                g_t.rx_task_max = std::max(g_t.rx_task_max, now_s() - tf);
+                g_t.rx_inflight_max = std::max(g_t.rx_inflight_max, rx.inflight());
                 if (closed && tasks.empty() && rx.inflight() == 0 && rx.pending() == 0) break;
             }
         } else {
@@ -435,6 +443,7 @@ int main(int argc, char** argv)
     g_noresident = argc > 5 && std::string(argv[5]) == "noresident";
     g_submitpoll = argc > 5 && std::string(argv[5]) == "submitpoll";
     if (argc > 5 && std::string(argv[5]) == "inflight2") g_inflight = 2;
+    if (argc > 5 && std::string(argv[5]) == "ring16m") g_tx_ring = (size_t)16 << 20;
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     const bool adapter = mode == "adapter";
     g_sync = mode == "sync";
@@ -459,7 +468,7 @@ int main(int argc, char** argv)
         if (adapter) {
             lo.rxloop = new kmws::RxLoop(nullptr, 0);
             if (!lo.rxloop->valid() || lo.rxloop->attachRing(lo.rring, kRing) != KMWS_OK) return 3;
-            lo.txloop = new kmws::TxLoop(nullptr, 0, (size_t)16 << 20, g_inflight);
+            lo.txloop = new kmws::TxLoop(nullptr, 0, g_tx_ring, g_inflight);
             if (!lo.txloop->valid()) return 3;
         } else if (kmws_rx_batch_attach_ring(lo.rx, lo.rring, kRing) != KMWS_OK) {
             return 3;
@@ -485,9 +494,10 @@ int main(int argc, char** argv)
                 "\"rx_flush_bytes\": %zu, \"best_of\": %d, \"GiB_s\": %.3f, \"us_per_frame\": %.3f, "
                 "\"verified\": %s, \"breakdown_ms_last_connection\": {\"client_total\": %.3f, "
                 "\"tx_flush\": %.3f, \"writev\": %.3f, \"server_recv\": %.3f, \"rx_feed\": %.3f, "
-                "\"rx_flush\": %.3f}}\n",
+                "\"rx_flush\": %.3f, \"rx_task_max\": %.3f, \"rx_wrap_flush\": %.3f, \"rx_wraps\": %d, \"rx_inflight_max\": %d}}\n",
                 mode.c_str(), kFrames, kLen, kGroup, kFlushBytes, reps, bytes / best / (1u << 30),
                 best / kFrames * 1e6, ok ? "true" : "false", g_t.client * 1e3, g_t.tx_flush * 1e3, g_t.writev * 1e3,
-                g_t.recv * 1e3, g_t.rx_feed * 1e3, g_t.rx_flush * 1e3);
+                g_t.recv * 1e3, g_t.rx_feed * 1e3, g_t.rx_flush * 1e3, g_t.rx_task_max * 1e3, g_t.rx_wrap * 1e3,
+                g_t.rx_wraps, g_t.rx_inflight_max);
     return ok ? 0 : 1;
 }

@@ -99,7 +99,8 @@ def loopback(reps: int):
                                "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", exe])
         for group in ("16", "64"):
             for mode, extra in (("cpu", []), ("sync", []), ("gpu", []), ("gpu", ["0", "noresident"]),
-                                ("gpu", ["0", "submitpoll"]), ("adapter", []), ("adapter", ["0", "inflight2"])):
+                                ("gpu", ["0", "submitpoll"]), ("adapter", []), ("adapter", ["0", "inflight2"]),
+                                ("adapter", ["0", "ring16m"])):
                 r = subprocess.run([exe, mode, str(reps), group] + extra, capture_output=True, text=True, timeout=300)
                 got = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
                 for x in got:
