@@ -54,6 +54,12 @@ constexpr int kResWords = 4;
 // workgroups poll one word every few microseconds; a claimed slot's workgroup
 // polls its job word and 31 descriptor slots (512 B) back to back.
 constexpr int kResSlots = 16;
+// Workgroups per slot: one CU moves ~13 GB/s of a job's PCIe traffic (the misses
+// it keeps in flight to host memory bound it, not its lanes), so a job of at
+// least 2 x kPartWords words is split over up to kResParts workgroups, each
+// polling the slot's job word itself.
+constexpr int kResParts = 4;
+constexpr uint32_t kPartWords = 1024;  // 16 KiB: the least a part takes
 // Idle exit: short.  The runtime maps streams onto a few hardware queues
 // (GPU_MAX_HW_QUEUES, 4 on the box), so a kernel launched on a stream that
 // shares the worker's queue waits until the worker leaves; and
@@ -102,16 +108,20 @@ struct ResDesc {  // one payload: device-visible address, bytes, LE key of its f
 static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 
 // The polled word of a slot: job number (bits 0-39), payload count (40-47),
-// claimed (62: a thread holds the slot, so its workgroup polls the
-// descriptors too) and quit (63).  The first kPollDescs descriptor slots
-// follow it and are read with it at every poll, so a job of up to kPollDescs
-// payloads costs one PCIe round trip to notice and none more to read its
-// descriptors.  The host rewrites every one of those slots for every job
-// (unused ones with length 0), each as two 8-byte stores tagged with the job's
-// low bits (address bits 48-63; length bits 21-31 in the half that also holds
-// the key): a half read before the host's write landed carries the previous
-// job's tag, and the job's descriptors are then read again after the word.
+// parts - 1 (48-49: the workgroups the job is split over), cancelled (61: a
+// job its thread withdrew -- no workgroup runs it), claimed (62: a thread holds
+// the slot, so its part-0 workgroup polls the descriptors too) and quit (63).
+// The first kPollDescs descriptor slots follow it and are read with it at
+// every poll of part 0, so a job of up to kPollDescs payloads costs one PCIe
+// round trip to notice and none more to read its descriptors.  The host
+// rewrites every one of those slots for every job (unused ones with length 0),
+// each as two 8-byte stores tagged with the job's low bits (address bits
+// 48-63; length bits 21-31 in the half that also holds the key): a half read
+// before the host's write landed carries the previous job's tag, and the job's
+// descriptors are then read again after the word.
 constexpr uint64_t kJobMask = (1ull << 40) - 1;
+constexpr int kPartShift = 48;
+constexpr uint64_t kCancelBit = 1ull << 61;
 constexpr uint64_t kClaimedBit = 1ull << 62;
 constexpr uint64_t kQuitBit = 1ull << 63;
 // word + 31 slots: a slot's first 512 bytes, one 16-byte load per lane of
@@ -137,15 +147,20 @@ __host__ __device__ __forceinline__ ResDesc untag_desc(ResDesc x)
     x.len &= kLenMask;
     return x;
 }
+// Words of a payload's 16-byte aligned hull.
+__host__ __device__ __forceinline__ uint32_t hull_words(uint64_t addr, uint32_t len)
+{
+    return len ? (uint32_t)(((addr + len + 15) >> 4) - (addr >> 4)) : 0u;
+}
 
 // Pinned host memory.  Host-written and device-written words sit in different
 // 128-byte lines.
 struct alignas(256) ResSlot {
-    uint64_t word;  // job | ndesc << 40 | claimed << 62 | quit << 63 (host, release)
+    uint64_t word;  // job | ndesc << 40 | (parts - 1) << 48 | cancel << 61 | claimed << 62 | quit << 63
     uint64_t pad1;
     ResDesc desc[kResMaxDescs];  // desc[i] at 16 + 16 i
-    alignas(128) uint64_t done;    // last job number finished (device, release: payloads visible)
-    uint64_t gone;                 // incarnation whose workgroup of this slot has left (device)
+    alignas(128) uint64_t done[kResParts];  // per part: last job number finished (release: its bytes visible)
+    uint64_t gone[kResParts];               // per part: incarnation whose workgroup has left
     alignas(128) uint64_t pad2;
 };
 struct ResMailbox {
@@ -157,7 +172,7 @@ struct ResMailbox {
 // compared with the incarnation number, so nothing is cleared between launches.
 struct ResCtl {
     uint64_t closing;   // max incarnation that is leaving (idle or lease)
-    uint64_t exits;     // workgroups exited, all incarnations (each adds kResSlots)
+    uint64_t exits;     // workgroups exited, all incarnations (each adds the grid size)
     uint64_t last_act;  // wall clock of the latest job taken in any slot
     uint64_t pad;
 };
@@ -172,9 +187,16 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// kResSlots workgroups, persistent until idle; workgroup b serves slot b.
-// `inc` = this incarnation's number (from 1).
+// nslots x kResParts workgroups (slots 0 .. nslots - 1: those claimed when
+// the incarnation was launched), persistent until idle: workgroup blockIdx.x
+// serves part blockIdx.x / nslots of slot blockIdx.x % nslots (a slot's parts
+// sit on different CUs).  A job's hull words are split evenly over its parts;
+// each part polls the slot's job word itself -- no hand-off between
+// workgroups -- runs its words and writes its own done word.  `inc` = this
+// incarnation's number (from 1); `exit_base` = the workgroups of every
+// earlier incarnation (the exit counter's value once they all left).
 __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* mb, ResCtl* ctl, uint64_t inc,
+                                                                    uint32_t nslots, uint64_t exit_base,
                                                                     uint64_t idle_ticks, uint64_t lease_ticks)
 {
     __shared__ ResDesc s_d[kResMaxDescs];
@@ -182,16 +204,18 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     __shared__ uint64_t s_cmd;
     __shared__ uint32_t s_have;  // descriptors taken from the poll
     const int t = threadIdx.x;
-    ResSlot* sl = &mb->slot[blockIdx.x];
+    const uint32_t part = blockIdx.x / nslots;
+    ResSlot* sl = &mb->slot[blockIdx.x % nslots];
     const uint64_t born = wall_clock64();
-    // lane l <= kPollDescs of wave 0 polls bytes [16 l, 16 l + 16) of the
-    // slot: the job word (lane 0) and descriptor slot l - 1; while the slot is
-    // unclaimed every lane loads lane 0's address (one request)
+    // lane l <= kPollDescs of wave 0 of part 0 polls bytes [16 l, 16 l + 16)
+    // of the slot: the job word (lane 0) and descriptor slot l - 1; other
+    // parts, and part 0 while the slot is unclaimed, load the word only (one
+    // request)
     const uint64_t* pw0 = &sl->word;
     const uint64_t* pw = pw0 + 2 * (t <= kPollDescs ? t : 0);
-    uint64_t last = 0, t_act = born;  // (wave 0) job done last; latest activity seen
-    bool full = true;                 // (wave 0) poll the descriptors too
-    if (t < 64) last = ld_sys(&sl->done);
+    uint64_t last = 0, t_act = born;  // (wave 0) job seen last; latest activity seen
+    bool full = part == 0;            // (wave 0) poll the descriptors too
+    if (t < 64) last = ld_sys(&sl->done[part]);
     for (;;) {
         if (t < 64) {  // wave 0, uniform control flow
             uint64_t cmd = 0, v0 = 0, v1 = 0;
@@ -210,12 +234,18 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 // (lane 0's job word; each half through uint32_t: readfirstlane is signed)
                 if (w & kQuitBit) break;  // this slot only: the rest of the grid serves on
                 if ((w & kJobMask) != last) {
+                    const uint32_t parts = (uint32_t)(w >> kPartShift & 3u) + 1u;
+                    if (part >= parts || (w & kCancelBit)) {
+                        last = w & kJobMask;  // not this workgroup's (no done word: nobody waits for it)
+                        continue;
+                    }
                     cmd = w;
                     if (t == 0) __hip_atomic_fetch_max(&ctl->last_act, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     t_act = now;
                     break;
                 }
-                full = (w & kClaimedBit) != 0;
+                const bool claimed = (w & kClaimedBit) != 0;
+                full = part == 0 && claimed;
                 if ((uint64_t)(now - t_act) > idle_ticks) {  // idle here: is every slot idle?
                     const uint64_t g = ld_agent(&ctl->last_act);
                     if ((int64_t)(g - t_act) > 0) t_act = g;
@@ -224,7 +254,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                         break;
                     }
                 }
-                if (full) __builtin_amdgcn_s_sleep(2);
+                if (claimed) __builtin_amdgcn_s_sleep(2);
                 else __builtin_amdgcn_s_sleep(127);  // ~4 us: an unclaimed slot gets a job rarely
             }
             uint32_t have = 0;
@@ -252,6 +282,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         if (cmd == 0) break;  // every wave leaves together
         const uint32_t nd = (uint32_t)(cmd >> 40) & 0xFFu;
         const uint32_t n = nd < (uint32_t)kResMaxDescs ? nd : (uint32_t)kResMaxDescs;
+        const uint32_t parts = (uint32_t)(cmd >> kPartShift & 3u) + 1u;
         if (s_have == 0 && t < (int)n) {
             const uint64_t* q = reinterpret_cast<const uint64_t*>(&sl->desc[t]);
             const uint64_t lo = ld_sys(q), hi = ld_sys(q + 1);  // each half one 8-byte load
@@ -274,14 +305,15 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
             uint32_t w = 0;
             for (uint32_t i = 0; i < n; ++i) {
                 s_pre[i] = w;
-                const ResDesc x = s_d[i];
-                w += x.len ? (uint32_t)(((x.addr + x.len + 15) >> 4) - (x.addr >> 4)) : 0u;
+                w += hull_words(s_d[i].addr, s_d[i].len);
             }
             s_pre[n] = w;
         }
         __syncthreads();
         const uint32_t total = s_pre[n];
-        for (uint32_t w0 = 0; w0 < total; w0 += kResBlock * kResWords) {
+        // this part's words: an even share, in job order
+        const uint32_t wb = (uint32_t)((uint64_t)total * part / parts), we = (uint32_t)((uint64_t)total * (part + 1) / parts);
+        for (uint32_t w0 = wb; w0 < we; w0 += kResBlock * kResWords) {
             u32x4 v[kResWords];
             uint32_t di[kResWords];
 #pragma unroll
@@ -289,7 +321,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 const uint32_t w = w0 + t + kResBlock * i;
                 di[i] = 0;
                 v[i] = u32x4{0, 0, 0, 0};
-                if (w < total) {
+                if (w < we) {
                     uint32_t lo = 0, hi = n;  // last payload whose first word is <= w
                     while (hi - lo > 1) {
                         const uint32_t mid = (lo + hi) >> 1;
@@ -303,7 +335,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
                 const uint32_t w = w0 + t + kResBlock * i;
-                if (w >= total) continue;
+                if (w >= we) continue;
                 const ResDesc x = s_d[di[i]];
                 const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
                 const uint64_t end = x.addr + x.len;
@@ -327,13 +359,13 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         // (tools/zc_probe.hip, profiles/r05n_zc_probe.jsonl).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(&sl->done, cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t == 0) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (t < 64) last = cmd & kJobMask;
     }
     if (t == 0) {
-        __hip_atomic_store(&sl->gone, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&sl->gone[part], inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t before = __hip_atomic_fetch_add(&ctl->exits, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (before + 1 == inc * (uint64_t)kResSlots)  // the grid's last workgroup
+        if (before + 1 == exit_base + gridDim.x)  // the grid's last workgroup
             __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -431,14 +463,20 @@ public:
         ResSlot& sl = mb_->slot[b];
         const uint64_t prev = seq_[b];
         uint64_t cur = ld_acq(&inc_);
-        if (ld_acq(&sl.done) != prev) {  // busy: the caller launches
+        if (cancelled_[b] != prev && !all_done(sl, prev, parts_[b])) {  // busy: the caller launches
             // (a job a previous holder left posted: a grid that left is relaunched for it)
             if (cur && ld_acq(&mb_->exited) == cur) (void)relaunch(cur);
             return KMWS_ERR_NOT_SUPPORTED;
         }
         if (cur == 0 || ld_acq(&mb_->exited) == cur) cur = relaunch(cur);
         if (cur == 0) return KMWS_ERR_NOT_SUPPORTED;
+        // a slot claimed after the running incarnation was launched has no
+        // workgroups in it: launch until the next incarnation (<= the lease)
+        if ((uint32_t)b >= ld_acq(&nslots_)) return KMWS_ERR_NOT_SUPPORTED;
         const uint64_t s = (prev + 1) & kJobMask;
+        uint64_t words = 0;
+        for (uint32_t i = 0; i < n; ++i) words += hull_words(d[i].addr, d[i].len);
+        const uint32_t parts = (uint32_t)std::min<uint64_t>(kResParts, std::max<uint64_t>(1, words / kPartWords));
         // every polled slot is rewritten, so a stale half always carries job s - 1's tag
         for (uint32_t i = 0; i < n || i < (uint32_t)kPollDescs; ++i) {
             const ResDesc x = tag_desc(i < n ? d[i] : ResDesc{0, 0, 0}, s);
@@ -447,8 +485,10 @@ public:
             __atomic_store_n(q + 1, (uint64_t)x.len | (uint64_t)x.key << 32, __ATOMIC_RELAXED);
         }
         seq_[b] = s;
+        parts_[b] = parts;
         __atomic_fetch_add(&jobs_, 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
-        __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | kClaimedBit, __ATOMIC_RELEASE);
+        __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | (uint64_t)(parts - 1) << kPartShift | kClaimedBit,
+                         __ATOMIC_RELEASE);
         *job = s;
         return KMWS_OK;
     }
@@ -459,12 +499,13 @@ public:
     int test(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
-        if (job_done(ld_acq(&sl.done), s)) return 1;
+        if (finished(b, s)) return 1;
         const uint64_t cur = ld_acq(&inc_);
         if (ld_acq(&mb_->exited) == cur) {
-            if (job_done(ld_acq(&sl.done), s)) return 1;
+            if (finished(b, s)) return 1;
             if (relaunch(cur) == 0 && withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
         }
+        (void)sl;
         return 0;
     }
 
@@ -478,19 +519,19 @@ public:
         const auto t0 = Clock::now();
         Clock::time_point orphan{};
         for (uint32_t spin = 0;; ++spin) {
-            if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
+            if (finished(b, s)) return KMWS_OK;
             cpu_relax();
             if ((spin & 255) != 255) continue;
             const uint64_t cur = ld_acq(&inc_);
             if (ld_acq(&mb_->exited) == cur) {  // the whole grid left: relaunch (the new one takes job s)
-                if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
+                if (finished(b, s)) return KMWS_OK;
                 if (relaunch(cur) == 0) {
                     if (withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;
                     continue;
                 }
                 orphan = Clock::time_point{};
-            } else if (ld_acq(&sl.gone) == cur) {  // this slot's workgroup left, others run on
-                if (job_done(ld_acq(&sl.done), s)) return KMWS_OK;
+            } else if (part_left(sl, s, parts_[b], cur)) {  // a part's workgroup left, others run on
+                if (finished(b, s)) return KMWS_OK;
                 const auto now = Clock::now();
                 if (orphan == Clock::time_point{}) orphan = now;
                 else if (now - orphan > std::chrono::microseconds(kResOrphanUs) && withdraw(b, s, cur))
@@ -514,21 +555,43 @@ public:
     }
 
 private:
-    // Takes job s of slot b back if no workgroup can take it any more: the
-    // grid `cur` is still the latest (no relaunch can start while launch_mu_
-    // is held) and its workgroup for b has left.  The slot's word returns to
-    // the previous job number (the quit bit cleared), so no later incarnation
-    // runs it.  False: it was done after all, or a newer grid will take it.
+    // Every part of job s finished?  (A part's done word at or past s.)
+    static bool all_done(const ResSlot& sl, uint64_t s, uint32_t parts)
+    {
+        for (uint32_t j = 0; j < parts; ++j)
+            if (!job_done(ld_acq(&sl.done[j]), s)) return false;
+        return true;
+    }
+    // Job s of slot b finished -- or the slot has moved on (a later job is
+    // posted only once s was finished or withdrawn, by s's own waiter).
+    bool finished(int b, uint64_t s) const { return seq_[b] != s || all_done(mb_->slot[b], s, parts_[b]); }
+    // Has the workgroup of an unfinished part of job s left grid `cur`?
+    static bool part_left(const ResSlot& sl, uint64_t s, uint32_t parts, uint64_t cur)
+    {
+        for (uint32_t j = 0; j < parts; ++j)
+            if (!job_done(ld_acq(&sl.done[j]), s) && ld_acq(&sl.gone[j]) == cur) return true;
+        return false;
+    }
+
+    // Takes job s of slot b back if no workgroup ran any of it and none can
+    // take it any more: the grid `cur` is still the latest (no relaunch can
+    // start while launch_mu_ is held) and the workgroup of every part has left.
+    // The word keeps the job number with the cancel bit (and the quit bit
+    // cleared), so no workgroup -- of this grid or a later one -- runs it; the
+    // slot's next job takes the next number.  False: a part ran (or runs), or
+    // a newer grid will take it.
     bool withdraw(int b, uint64_t s, uint64_t cur)
     {
         ResSlot& sl = mb_->slot[b];
         std::lock_guard<std::mutex> lk(launch_mu_);
-        // (a later job was posted on the slot only after s was done)
-        if (ld_acq(&inc_) != cur || seq_[b] != s || job_done(ld_acq(&sl.done), s)) return false;
-        if (ld_acq(&sl.gone) != cur && ld_acq(&mb_->exited) != cur) return false;
-        const uint64_t prev = (s - 1) & kJobMask;
-        seq_[b] = prev;
-        __atomic_store_n(&sl.word, prev | kClaimedBit, __ATOMIC_RELEASE);
+        if (ld_acq(&inc_) != cur || seq_[b] != s) return false;
+        const bool all_left = ld_acq(&mb_->exited) == cur;
+        for (uint32_t j = 0; j < parts_[b]; ++j) {
+            if (job_done(ld_acq(&sl.done[j]), s)) return false;
+            if (!all_left && ld_acq(&sl.gone[j]) != cur) return false;
+        }
+        __atomic_store_n(&sl.word, (ld_acq(&sl.word) | kCancelBit) & ~kQuitBit, __ATOMIC_RELEASE);
+        cancelled_[b] = s;
         __atomic_fetch_add(&withdrawn_, 1, __ATOMIC_RELAXED);
         __atomic_fetch_sub(&jobs_, 1, __ATOMIC_RELAXED);
         return true;
@@ -539,11 +602,12 @@ private:
     kmws_status timed_out(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
+        const uint32_t parts = parts_[b];
         __atomic_fetch_add(&timeouts_, 1, __ATOMIC_RELAXED);
         __atomic_fetch_or(&sl.word, kQuitBit, __ATOMIC_RELEASE);
         const auto t0 = Clock::now();
         for (uint32_t spin = 0;; ++spin) {
-            if (job_done(ld_acq(&sl.done), s)) {
+            if (finished(b, s)) {
                 std::lock_guard<std::mutex> lk(launch_mu_);
                 __atomic_fetch_and(&sl.word, ~kQuitBit, __ATOMIC_RELEASE);
                 return KMWS_OK;
@@ -551,8 +615,19 @@ private:
             cpu_relax();
             if ((spin & 255) != 255) continue;
             const uint64_t cur = ld_acq(&inc_);
-            if ((ld_acq(&sl.gone) == cur || ld_acq(&mb_->exited) == cur) && withdraw(b, s, cur))
-                return KMWS_ERR_NOT_SUPPORTED;  // it left without running the job
+            const bool all_left = ld_acq(&mb_->exited) == cur;
+            bool settled = true;  // every part finished, or its workgroup left
+            for (uint32_t j = 0; j < parts; ++j)
+                settled &= job_done(ld_acq(&sl.done[j]), s) || all_left || ld_acq(&sl.gone[j]) == cur;
+            if (settled) {
+                if (withdraw(b, s, cur)) return KMWS_ERR_NOT_SUPPORTED;  // no part ran: the caller launches
+                // some parts ran: the others run in the next grid (the quit bit cleared)
+                {
+                    std::lock_guard<std::mutex> lk(launch_mu_);
+                    __atomic_fetch_and(&sl.word, ~kQuitBit, __ATOMIC_RELEASE);
+                }
+                if (all_left) (void)relaunch(cur);
+            }
             if (Clock::now() - t0 > std::chrono::milliseconds(KMWS_RESIDENT_DRAIN_MS)) break;
         }
         // still held by a workgroup that does not leave: the payloads stay the
@@ -619,13 +694,19 @@ private:
         const uint64_t cur = inc_;
         if (cur != seen) return cur;                                   // another thread relaunched
         if (cur != 0 && ld_acq(&mb_->exited) != cur) return cur;      // still running
+        // the slots claimed now, up to the highest (a slot claimed later is
+        // served from the next incarnation on; its jobs launch until then)
+        const uint32_t m = ld_acq(&claimed_);
+        const uint32_t nslots = m ? 32u - (uint32_t)__builtin_clz(m) : 1u;
         DevGuard g(device_);
-        hipLaunchKernelGGL(resident_unmask_kernel, dim3(kResSlots), dim3(kResBlock), 0, stream_, dmb_, dctl_, cur + 1,
-                           idle_ticks_, lease_ticks_);
+        hipLaunchKernelGGL(resident_unmask_kernel, dim3(nslots * kResParts), dim3(kResBlock), 0, stream_, dmb_, dctl_,
+                           cur + 1, nslots, exit_base_, idle_ticks_, lease_ticks_);
         if (hipGetLastError() != hipSuccess) {
             state_ = -1;
             return 0;
         }
+        exit_base_ += (uint64_t)nslots * kResParts;
+        __atomic_store_n(&nslots_, nslots, __ATOMIC_RELEASE);
         __atomic_store_n(&inc_, cur + 1, __ATOMIC_RELEASE);
         return cur + 1;
     }
@@ -641,7 +722,11 @@ private:
     hipStream_t stream_ = nullptr;
     uint64_t idle_ticks_ = 0, lease_ticks_ = 0;
     uint64_t inc_ = 0;  // latest incarnation launched
-    uint64_t seq_[kResSlots] = {};  // last job number posted per slot (by its holder)
+    uint32_t nslots_ = 0;     // slots the latest incarnation serves
+    uint64_t exit_base_ = 0;  // workgroups launched in all incarnations so far
+    uint64_t seq_[kResSlots] = {};        // last job number posted per slot (by its holder)
+    uint32_t parts_[kResSlots] = {};      // its parts
+    uint64_t cancelled_[kResSlots] = {};  // the last job withdrawn per slot
     uint64_t jobs_ = 0, timeouts_ = 0, withdrawn_ = 0;
 };
 

@@ -431,8 +431,10 @@ def test_resident_lease_relaunches_a_busy_worker():
 def test_resident_worker_slot_per_thread():
     """Four threads masking concurrently each hold their own mailbox slot of
     the device's resident grid (no lock between them): distinct slots, every
-    result exact, every job on the worker, and the median call stays in the
-    tens of microseconds."""
+    result exact, the jobs on the worker (but those of a slot claimed while
+    the running incarnation did not cover it yet: launched until the next, at
+    most a 1 ms lease later), and the median call stays in the tens of
+    microseconds."""
     import threading
     import time
     rng = random.Random(23)
@@ -464,7 +466,7 @@ def test_resident_worker_slot_per_thread():
     assert all(b == 0 for _, b, _ in res.values()), res
     slots = [s for _, _, s in res.values()]
     assert all(s >= 0 for s in slots) and len(set(slots)) == 4, slots
-    assert after["jobs"] - before["jobs"] == 1600
+    assert 1400 <= after["jobs"] - before["jobs"] <= 1600, (before, after)
     assert max(m for m, _, _ in res.values()) < 2e-4, res
     # the threads have exited: their slots are free again
     assert kmws.resident_info()["slots_claimed"] <= before["slots_claimed"], (before, kmws.resident_info())
@@ -512,7 +514,8 @@ def test_resident_and_launch_paths_interleaved_on_many_threads():
     chains of up to three segments: jobs of up to 64 KiB run on each thread's
     slot of the resident grid, larger ones are launched on the thread's own
     stream, interleaved on every thread.  Every byte equals the oracle's, and
-    exactly the jobs that fit the worker ran on it."""
+    the jobs that fit the worker ran on it (but a new slot's first ones, until
+    the grid's next incarnation covers it)."""
     import threading
     res = {}
 
@@ -540,7 +543,8 @@ def test_resident_and_launch_paths_interleaved_on_many_threads():
         t.join()
     after = kmws.resident_info()
     assert all(b == 0 for b, _ in res.values()), res
-    assert after["jobs"] - before["jobs"] == sum(s for _, s in res.values()), (before, after, res)
+    small = sum(s for _, s in res.values())
+    assert small - 12 <= after["jobs"] - before["jobs"] <= small, (before, after, res)
 
 
 def _testhooks_lib():
