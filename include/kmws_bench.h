@@ -57,12 +57,13 @@ kmws_status kmws_check_unmasked(const uint8_t* base, uint64_t bytes, uint64_t se
                                 const kmws_desc* descs, uint32_t n,
                                 unsigned long long* mismatches, void* stream);
 
-/* The resident worker on `device` (kmws_resident.hip): one grid per device of
- * 16 workgroups, one per mailbox slot; a host thread claims a slot at its first
- * job and keeps it until it exits, so up to 16 loop threads run their jobs at
- * once (a thread finding no free slot launches instead).  It serves the host
+/* The resident worker on `device` (kmws_resident.hip): one grid per device, up
+ * to 16 mailbox slots of four workgroups each (a job's parts); a host thread
+ * claims a slot at its first job and keeps it until it exits, so up to 16 loop
+ * threads run their jobs at once (a thread finding no free slot launches
+ * instead; an incarnation serves the slots claimed when it started).  It serves the host
  * entries' small jobs (kmws_decoder_feed, kmws_mask_host_chain, rx / tx batch
- * flushes and submits; <= 128 payloads and <= 64 KiB) without a launch per
+ * flushes and submits; <= 128 payloads and <= 256 KiB) without a launch per
  * call.  enable(0) makes the CALLING thread's calls launch a kernel per call
  * instead (the A/B of bench.py cfg1) and gives its slot back; info: jobs
  * served, launches (incarnations) so far, and whether it is on the GPU now (it

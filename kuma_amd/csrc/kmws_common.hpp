@@ -101,14 +101,12 @@ kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const Pi
 // payloads and kResMaxBytes bytes go to the calling thread's slot of a grid
 // that stays on the GPU polling pinned memory, instead of a launch per call.
 constexpr int kResMaxDescs = 128;
-// One workgroup moves a job over PCIe at ~3 GB/s: at 64 KiB it is as fast as a
-// launch of the multi-block pieces kernel (20 us each, tests/cpp/rx_flush_bench.cpp,
-// profiles/r04w_rx_flush_bench.jsonl), below it faster (10.7 vs 18.5 us at 16
-// KiB); above it the launch's several blocks move the bytes faster.
-constexpr uint64_t kResMaxBytes = 64u << 10;
-// An asynchronous job (an rx / tx batch's submit) costs the loop thread no
-// launch however long it runs; up to this size it goes to the worker too.
-constexpr uint64_t kResMaxBytesAsync = 256u << 10;
+// A job runs on up to four workgroups of its slot (one per 16 KiB of hull
+// words): 256 KiB take ~11 us on the device (tools/zc_probe.hip), a launch of
+// the pieces kernel alone ~20 us.  Synchronous (a flush, a feed, a mask) and
+// asynchronous jobs (an rx / tx batch's submit) alike.
+constexpr uint64_t kResMaxBytes = 256u << 10;
+constexpr uint64_t kResMaxBytesAsync = kResMaxBytes;
 struct ResidentJob {
     int device = -1;
     int slot = -1;

@@ -511,7 +511,7 @@ def test_resident_more_threads_than_slots_launch_instead():
 
 def test_resident_and_launch_paths_interleaved_on_many_threads():
     """Four threads at once, 40 jobs each of 1 B to 512 KiB at odd offsets,
-    chains of up to three segments: jobs of up to 64 KiB run on each thread's
+    chains of up to three segments: jobs of up to 256 KiB run on each thread's
     slot of the resident grid, larger ones are launched on the thread's own
     stream, interleaved on every thread.  Every byte equals the oracle's, and
     the jobs that fit the worker ran on it (but a new slot's first ones, until
@@ -532,7 +532,7 @@ def test_resident_and_launch_paths_interleaved_on_many_threads():
             want = orc.mask_bytes(key, data[off:off + n])
             kmws.handle_data_mask(key, segs)
             bad += b"".join(segs) != want
-            small += n <= 65536
+            small += n <= 262144
         res[tid] = (bad, small)
 
     before = kmws.resident_info()
@@ -646,10 +646,11 @@ def test_resident_timeout_past_drain_returns_timeout_status():
     assert bytes(a) == data
 
 
-@pytest.mark.parametrize("n", [1, 3, 15, 16, 17, 1024, 4096, 65536, 65537, 300000, (1 << 20) + 5])
+@pytest.mark.parametrize("n", [1, 3, 15, 16, 17, 1024, 4096, 16384, 16385, 65536, 65537, 262144, 262145, 300000,
+                               (1 << 20) + 5])
 def test_mask_host_chain_sizes_resident_and_launch(n):
     """handleDataMask(key, data, len) at every size class through the resident
-    worker (<= 64 KiB) and beyond it (the launch path), against the oracle's
+    grid (<= 256 KiB: one to four parts) and beyond it (the launch path), against the oracle's
     byte loop, at odd alignments inside a larger buffer."""
     rng = random.Random(n)
     key = bytes(rng.randrange(256) for _ in range(4))
