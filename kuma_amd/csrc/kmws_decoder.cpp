@@ -82,7 +82,12 @@ struct kmws_decoder {
     }
 };
 
+// Stages a batch makes before its first loop iteration (a generation in
+// flight each; more are made if needed).
+constexpr int kWarmStages = 4;
+
 struct kmws_rx_batch {
+    BatchStream bstream;  // first: destroyed after every stage that uses it
     struct Item {
         kmws_decoder* dec;  // identity only; never dereferenced at delivery
         kmws_frame_cb cb;
@@ -118,8 +123,21 @@ struct kmws_rx_batch {
             return s;
         }
         std::unique_ptr<PinnedStage> s(new (std::nothrow) PinnedStage());
-        if (s && s->init(device) != KMWS_OK) s.reset();
+        if (s && s->init(device, bstream.s) != KMWS_OK) s.reset();
         return s;
+    }
+    // the stream and a few warm stages, made before the first loop iteration
+    kmws_status prepare(int dev)
+    {
+        device = dev;
+        kmws_status st = bstream.create(dev);
+        for (int i = 0; st == KMWS_OK && i < kWarmStages; ++i) {
+            std::unique_ptr<PinnedStage> s = take_stage();
+            if (!s) return KMWS_ERR_FAILED;
+            st = s->warm();
+            spare.push_back(std::move(s));
+        }
+        return st;
     }
 };
 
@@ -503,6 +521,7 @@ void kmws_host_free(void* p)
 // next generation meanwhile.  kmws_tx_batch_flush = submit + poll(wait).
 
 struct kmws_tx_batch {
+    BatchStream bstream;  // first: destroyed after every stage that uses it
     struct Seg {
         uint8_t* p;
         size_t len;
@@ -542,8 +561,21 @@ struct kmws_tx_batch {
             return s;
         }
         std::unique_ptr<PinnedStage> s(new (std::nothrow) PinnedStage());
-        if (s && s->init(device) != KMWS_OK) s.reset();
+        if (s && s->init(device, bstream.s) != KMWS_OK) s.reset();
         return s;
+    }
+    // the stream and a few warm stages, made before the first loop iteration
+    kmws_status prepare(int dev)
+    {
+        device = dev;
+        kmws_status st = bstream.create(dev);
+        for (int i = 0; st == KMWS_OK && i < kWarmStages; ++i) {
+            std::unique_ptr<PinnedStage> s = take_stage();
+            if (!s) return KMWS_ERR_FAILED;
+            st = s->warm();
+            spare.push_back(std::move(s));
+        }
+        return st;
     }
 };
 
@@ -551,7 +583,10 @@ kmws_tx_batch* kmws_tx_batch_create(int device)
 {
     kmws_tx_batch* b = new (std::nothrow) kmws_tx_batch();
     if (!b) return nullptr;
-    b->device = device;
+    if (b->prepare(device) != KMWS_OK) {
+        delete b;
+        return nullptr;
+    }
     b->stage = b->take_stage();
     if (!b->stage) {
         delete b;
@@ -724,7 +759,10 @@ kmws_rx_batch* kmws_rx_batch_create(int device)
 {
     kmws_rx_batch* b = new (std::nothrow) kmws_rx_batch();
     if (!b) return nullptr;
-    b->device = device;
+    if (b->prepare(device) != KMWS_OK) {
+        delete b;
+        return nullptr;
+    }
     b->stage = b->take_stage();
     if (!b->stage) {
         delete b;

@@ -63,11 +63,37 @@ inline size_t grow(size_t need, size_t have)
 // batch of descriptors can target another pinned buffer (a caller's registered
 // receive or send ring).  The asynchronous rx / tx batches keep one stage per
 // generation in flight (kmws_decoder.cpp).
+// A stream a batch owns and its stages share; declared first in the batch so
+// it is destroyed after every stage.
+struct BatchStream {
+    hipStream_t s = nullptr;
+    int device = -1;
+    kmws_status create(int dev)
+    {
+        device = dev;
+        if (dev < 0 || kmws_device_count() <= dev) return KMWS_ERR_NOT_SUPPORTED;
+        DevGuard g(dev);
+        return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? KMWS_OK : KMWS_ERR_FAILED;
+    }
+    ~BatchStream()
+    {
+        if (!s) return;
+        DevGuard g(device);
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
+};
+
 class PinnedStage {
 public:
     ~PinnedStage() { release(); }
 
-    kmws_status init(int device)
+    // shared: a stream the owner keeps for all its stages (a batch's
+    // generations), else the stage creates its own.  Creating a stream can
+    // take milliseconds -- a loop iteration that needed a new stage stalled
+    // for 2-3.5 ms (r05i/r05j loopback, rx_task_max) -- so the batches create
+    // theirs once.
+    kmws_status init(int device, hipStream_t shared = nullptr)
     {
         if (dev_ok_ < 0) {
             device_ = device;
@@ -76,13 +102,27 @@ public:
         if (!dev_ok_) return KMWS_ERR_NOT_SUPPORTED;
         if (!stream_) {
             DevGuard g(device_);
-            if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return KMWS_ERR_FAILED;
+            if (shared) {
+                stream_ = shared;
+                own_stream_ = false;
+            } else if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+                return KMWS_ERR_FAILED;
+            }
             if (hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess) return KMWS_ERR_FAILED;
         }
         return KMWS_OK;
     }
     int device() const { return device_; }
     hipStream_t stream() const { return stream_; }
+
+    // Allocates the pinned staging area and descriptor / piece arrays ahead
+    // of use (hipHostMalloc can take milliseconds inside a loop iteration).
+    kmws_status warm()
+    {
+        kmws_status st = reserve(64u << 10);
+        if (st == KMWS_OK) st = ensure_host(kResMaxDescs, 4 * kResMaxDescs);
+        return st;
+    }
 
     // Room for `bytes` more payload bytes (plus alignment) without moving offsets.
     kmws_status reserve(size_t bytes)
@@ -335,17 +375,18 @@ private:
     void release()
     {
         if (launched_) (void)wait();  // nothing may outlive its pinned memory (a timed-out job's is abandoned)
-        if (stream_) (void)hipStreamSynchronize(stream_);
+        if (stream_ && own_stream_) (void)hipStreamSynchronize(stream_);
         if (done_) (void)hipEventDestroy(done_);
         if (h_) (void)hipHostFree(h_);
         if (h_desc_) (void)hipHostFree(h_desc_);
         if (h_piece_) (void)hipHostFree(h_piece_);
-        if (stream_) (void)hipStreamDestroy(stream_);
+        if (stream_ && own_stream_) (void)hipStreamDestroy(stream_);
     }
 
     int device_ = 0;
     int dev_ok_ = -1;
     hipStream_t stream_ = nullptr;
+    bool own_stream_ = true;
     hipEvent_t done_ = nullptr;
     bool launched_ = false;
     bool res_pending_ = false;  // launched_ on the resident worker: res_ says which job
