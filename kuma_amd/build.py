@@ -55,12 +55,13 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     if out is None and not force and up_to_date():
         return LIB
     lib = out or LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
+    obj_dir = os.path.dirname(os.path.abspath(lib))  # beside the output: variant builds never share objects
+    os.makedirs(obj_dir, exist_ok=True)
     objs = []
     inc = ["-I", os.path.join(ROOT, "include"), "-I", srcdir or os.path.join(HERE, "csrc")]
     cmds = []
     for src in sources(srcdir):
-        obj = os.path.join(LIB_DIR, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
         cmds.append(["hipcc", "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                      "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines], *inc, "-c", src, "-o", obj])
         objs.append(obj)

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -67,11 +68,10 @@ struct kmws_decoder {
     St state = St::HDR1;
     std::vector<uint8_t> buf;
     uint8_t pos = 0;
-    // synchronous-feed delivery lists and staging
+    // synchronous-feed delivery lists (the staging is borrowed per call: StagePool)
     std::vector<Pending> pending;
     std::vector<std::vector<uint8_t>> held;
     std::vector<kmws_desc> chunk_descs;
-    PinnedStage stage;
 
     void reset_ctx()  // DecodeContext::reset, WSHandler.h:66-72 (capacity kept)
     {
@@ -142,6 +142,78 @@ struct kmws_rx_batch {
 };
 
 namespace {
+
+// Pinned stages for the synchronous entries (kmws_decoder_feed,
+// kmws_mask_host_chain), shared by every connection and thread of the process.
+// A stage is used only within one call -- its payloads are unmasked and
+// delivered before the call returns -- so a call borrows one and gives it back;
+// a callback that feeds another decoder borrows another.  The pool holds as
+// many stages as calls ever ran at once, each with its stream, event and
+// pinned area made once: a decoder per connection (kuma's WSHandler) would
+// otherwise create a stream (milliseconds) and 1 MiB of pinned memory per
+// connection, and a new loop thread its own.  Never freed (pinned memory must
+// not be released after the HIP runtime's teardown at process exit).
+class StagePool {
+public:
+    PinnedStage* take(int device, kmws_status* st)
+    {
+        *st = KMWS_OK;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (size_t i = free_.size(); i-- > 0;)  // the most recently used first (warm in cache)
+                if (free_[i]->device() == device) {
+                    PinnedStage* s = free_[i];
+                    free_.erase(free_.begin() + (ptrdiff_t)i);
+                    return s;
+                }
+        }
+        PinnedStage* s = new (std::nothrow) PinnedStage();
+        if (!s) {
+            *st = KMWS_ERR_FAILED;
+            return nullptr;
+        }
+        *st = s->init(device);  // KMWS_ERR_NOT_SUPPORTED: no such gfx950 device
+        if (*st == KMWS_OK) *st = s->warm();
+        if (*st != KMWS_OK) {
+            delete s;
+            s = nullptr;
+        }
+        return s;
+    }
+    void give(PinnedStage* s)
+    {
+        s->clear();
+        std::lock_guard<std::mutex> lk(mu_);
+        free_.push_back(s);
+    }
+
+private:
+    std::mutex mu_;
+    std::vector<PinnedStage*> free_;
+};
+
+StagePool& stage_pool()
+{
+    static StagePool* p = new StagePool();
+    return *p;
+}
+
+// A stage borrowed for the scope of one call (taken at first use).
+struct BorrowedStage {
+    int device;
+    PinnedStage* s = nullptr;
+    kmws_status st = KMWS_OK;  // why get() failed
+    explicit BorrowedStage(int dev) : device(dev) {}
+    ~BorrowedStage()
+    {
+        if (s) stage_pool().give(s);
+    }
+    PinnedStage* get()
+    {
+        if (!s) s = stage_pool().take(device, &st);
+        return s;
+    }
+};
 
 // The reference's decodeFrame loop (WSHandler.cpp:108-280).  At every
 // completed frame, sink(hdr, payload, reassembly) is called with the payload
@@ -341,7 +413,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     dec->pending.clear();
     dec->held.clear();
     dec->chunk_descs.clear();
-    dec->stage.clear();
+    BorrowedStage bs(dec->device);  // given back when the call returns (the decoder may be gone by then)
     int chunk_pinned = -1;  // resolved at the first masked in-chunk frame
     uint8_t* chunk_dv = nullptr;
     uint8_t* chunk_base = reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(data) & ~(uintptr_t)15);
@@ -352,10 +424,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
         const bool masked = h.mask && h.length;  // handleDataMask is a no-op otherwise (:293, :305)
         uint32_t key;
         std::memcpy(&key, h.maskey, 4);
-        if (masked) {
-            kmws_status st = dec->stage.init(dec->device);
-            if (st != KMWS_OK) return st;
-        }
+        if (masked && !bs.get()) return bs.st;
         if (!reasm) {
             q.data_ptr = payload;
             if (!masked) {
@@ -371,18 +440,18 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
                     dec->chunk_descs.push_back(kmws_desc{(uint64_t)(payload - chunk_base), h.length, key});
                     q.where = kInChunkPinned;
                 } else {
-                    kmws_status st = dec->stage.reserve(h.length);
+                    kmws_status st = bs.s->reserve(h.length);
                     if (st != KMWS_OK) return st;
-                    q.stage_off = dec->stage.append(payload, h.length);
-                    dec->stage.add_desc(q.stage_off, h.length, key);
+                    q.stage_off = bs.s->append(payload, h.length);
+                    bs.s->add_desc(q.stage_off, h.length, key);
                     q.where = kInChunkStaged;
                 }
             }
         } else if (masked) {
-            kmws_status st = dec->stage.reserve(h.length);
+            kmws_status st = bs.s->reserve(h.length);
             if (st != KMWS_OK) return st;
-            q.stage_off = dec->stage.append(payload, h.length);
-            dec->stage.add_desc(q.stage_off, h.length, key);
+            q.stage_off = bs.s->append(payload, h.length);
+            bs.s->add_desc(q.stage_off, h.length, key);
             q.where = kStagedMasked;
         } else {
             dec->held.emplace_back();
@@ -398,9 +467,9 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     if (result < 0) return result;
 
     // ---- GPU unmask of every masked payload of this call ----
-    if (dec->stage.n_desc() || !dec->chunk_descs.empty()) {
+    if (bs.s && (bs.s->n_desc() || !dec->chunk_descs.empty())) {
         const uint64_t chunk_span = (uint64_t)((data + len) - chunk_base);
-        kmws_status st = dec->stage.run(chunk_base, chunk_span, &dec->chunk_descs, chunk_dv);
+        kmws_status st = bs.s->run(chunk_base, chunk_span, &dec->chunk_descs, chunk_dv);
         if (st != KMWS_OK) return st;
     }
 
@@ -410,7 +479,7 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
     todo.swap(dec->pending);
     std::vector<std::vector<uint8_t>> held;
     held.swap(dec->held);
-    uint8_t* stage = dec->stage.data();
+    uint8_t* stage = bs.s ? bs.s->data() : nullptr;
     for (Pending& q : todo) {
         uint8_t* payload;
         switch (q.where) {
@@ -435,20 +504,6 @@ int kmws_decoder_feed(kmws_decoder* dec, uint8_t* data, size_t len, kmws_frame_c
 
 // ---- host-buffer masking: WSHandler::handleDataMask statics (a-1, a-2) ----
 
-namespace {
-// One staging area per device and loop thread for the synchronous host mask
-// entry.  Never freed: releasing pinned memory from a thread_local destructor
-// can run after the HIP runtime has been torn down at process exit.
-PinnedStage* tx_stage(int device)
-{
-    static thread_local std::vector<PinnedStage*>* by_dev = new std::vector<PinnedStage*>();
-    if (device < 0) return nullptr;
-    if ((size_t)device >= by_dev->size()) by_dev->resize(device + 1, nullptr);
-    if (!(*by_dev)[device]) (*by_dev)[device] = new (std::nothrow) PinnedStage();
-    return (*by_dev)[device];
-}
-}  // namespace
-
 // Masks a chain of host segments in place with the key phase continuing across
 // segments (WSHandler.cpp:312-322; one segment = :303-310).  The segments are
 // gathered back to back into pinned staging -- so the chain is one payload and
@@ -464,12 +519,11 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
     }
     if (total == 0) return KMWS_OK;  // nothing to do (:305)
     if (total > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
-    PinnedStage* s = tx_stage(device);
-    if (!s) return KMWS_ERR_INVALID_PARAM;
-    kmws_status st = s->init(device);
-    if (st != KMWS_OK) return st;
-    s->clear();
-    st = s->reserve(total);
+    if (device < 0) return KMWS_ERR_INVALID_PARAM;
+    BorrowedStage bs(device);  // a stage of the process's pool for this call (StagePool)
+    PinnedStage* s = bs.get();
+    if (!s) return bs.st;
+    kmws_status st = s->reserve(total);
     if (st != KMWS_OK) return st;
     size_t off = 0;
     uint8_t* dst = s->alloc(total, &off);
@@ -488,7 +542,6 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
         if (lens[i]) std::memcpy(segs[i], dst + pos, lens[i]);
         pos += lens[i];
     }
-    s->clear();
     return KMWS_OK;
 }
 

@@ -31,15 +31,19 @@
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [variant]
+// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [variant] [connections]
 // (variant noresident: both loop threads switch their resident worker off --
 // every GPU job a launch and a wait, the A/B of kmws_resident.hip; submitpoll:
 // the gpu mode's flushes replaced by submit + poll(wait); inflight2: the
 // adapter's TxLoop keeps two generations in flight instead of one; ring16m: its
-// send ring is 16 MiB instead of 1 MiB)
+// send ring is 16 MiB instead of 1 MiB; "0" or "-": none).  connections (1-8): that many
+// client / server loop-thread pairs at once, each with its own connection and loop
+// objects, 1,000 frames each; GiB_s is the aggregate from the first send of any
+// connection to the last frame delivered on any (kuma runs several loop threads)
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -93,6 +97,13 @@ uint64_t splitmix(uint64_t x)
     return z ^ (z >> 31);
 }
 
+double cpu_s()  // CPU time of every thread of the process so far (user + system)
+{
+    rusage u{};
+    getrusage(RUSAGE_SELF, &u);
+    return (double)u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6;
+}
+
 double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -101,6 +112,7 @@ struct Times {  // seconds spent per step in the last connection (breakdown)
     double tx_flush = 0, writev = 0, rx_feed = 0, rx_flush = 0, recv = 0, client = 0;
     double rx_task_max = 0, rx_wrap = 0;  // adapter: the longest posted rx task; flushes at ring wraps
     int rx_wraps = 0, rx_inflight_max = 0;
+    double t0 = 0, t_end = 0;  // this connection's first send and last delivered frame (steady clock)
 } g_t;
 
 struct Expect {
@@ -169,7 +181,8 @@ bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flus
 int g_inflight = 1;         // adapter mode: the TxLoop's generations in flight after a run (inflight2: 2)
 size_t g_tx_ring = (size_t)1 << 20;  // adapter mode: the TxLoop's pinned send ring (ring16m: 16 MiB)
 
-double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo)
+double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& keys, const LoopObjs& lo, Times& T,
+                std::atomic<int>* gate = nullptr, int conns = 1)
 {
     int ls = socket(AF_INET, SOCK_STREAM, 0);
     sockaddr_in a{};
@@ -183,7 +196,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     }
     e.got = 0;
     e.bad = 0;
-    g_t = Times();
+    T = Times();
     std::atomic<bool> ready{false};
     std::chrono::steady_clock::time_point t_end;
 
@@ -205,11 +218,11 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             while (e.got.load(std::memory_order_acquire) < kFrames) {
                 double t = now_s();
                 const ssize_t r = recv(fd, buf.data(), kRead, 0);
-                g_t.recv += now_s() - t;
+                T.recv += now_s() - t;
                 if (r <= 0) break;
                 t = now_s();
                 const kmws::ws::WSError err = h.handleData(buf.data(), (size_t)r);
-                g_t.rx_feed += now_s() - t;
+                T.rx_feed += now_s() - t;
                 if (err != kmws::ws::WSError::NOERR && err != kmws::ws::WSError::NEED_MORE_DATA) std::exit(4);
             }
         } else if (gpu && !adapter) {
@@ -226,12 +239,12 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                     if (pos + kRead > kRing) break;  // ring full: flush first
                     double t = now_s();
                     const ssize_t r = recv(fd, ring + pos, kRead, flags);
-                    g_t.recv += now_s() - t;
+                    T.recv += now_s() - t;
                     if (r == 0) closed = true;
                     if (r <= 0) break;
                     t = now_s();
                     if (kmws_decoder_feed_deferred(d, b, ring + pos, (size_t)r, kmws_cb, &e) < 0) std::exit(4);
-                    g_t.rx_feed += now_s() - t;
+                    T.rx_feed += now_s() - t;
                     pos += (size_t)r;
                     flags = MSG_DONTWAIT;
                 }
@@ -246,7 +259,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 } else if (kmws_rx_batch_flush(b) < 0) {
                     std::exit(5);
                 }
-                g_t.rx_flush += now_s() - tf;
+                T.rx_flush += now_s() - tf;
                 pos = 0;  // ring bytes are free again after the flush
             }
             kmws_decoder_destroy(d);
@@ -274,19 +287,19 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                     if (pos + kRead > kRing) {  // wrap: ring bytes are free once every frame was delivered
                         const double tf = now_s();
                         if (rx.flush() < 0) std::exit(5);
-                        g_t.rx_flush += now_s() - tf;
-                        g_t.rx_wrap += now_s() - tf;
-                        ++g_t.rx_wraps;
+                        T.rx_flush += now_s() - tf;
+                        T.rx_wrap += now_s() - tf;
+                        ++T.rx_wraps;
                         pos = 0;
                     }
                     double t = now_s();
                     const ssize_t r = closed ? -1 : recv(fd, ring + pos, kRead, flags);
-                    g_t.recv += now_s() - t;
+                    T.recv += now_s() - t;
                     if (r == 0) closed = true;
                     if (r <= 0) break;
                     t = now_s();
                     const kmws::ws::WSError err = h.handleData(ring + pos, (size_t)r);  // onWsData
-                    g_t.rx_feed += now_s() - t;
+                    T.rx_feed += now_s() - t;
                     if (err != kmws::ws::WSError::NOERR && err != kmws::ws::WSError::NEED_MORE_DATA) std::exit(4);
                     pos += (size_t)r;
                     flags = MSG_DONTWAIT;
@@ -296,9 +309,9 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 now.swap(tasks);
                 for (auto& t : now) t();
                 if (rx.lastResult() < 0) std::exit(5);
-                g_t.rx_flush += now_s() - tf;
-                g_t.rx_task_max = std::max(g_t.rx_task_max, now_s() - tf);
-                g_t.rx_inflight_max = std::max(g_t.rx_inflight_max, rx.inflight());
+                T.rx_flush += now_s() - tf;
+                T.rx_task_max = std::max(T.rx_task_max, now_s() - tf);
+                T.rx_inflight_max = std::max(T.rx_inflight_max, rx.inflight());
                 if (closed && tasks.empty() && rx.inflight() == 0 && rx.pending() == 0) break;
             }
         } else {
@@ -323,6 +336,10 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     while (!ready) std::this_thread::yield();
+    if (gate) {  // several connections at once: every one connected before any sends
+        gate->fetch_add(1);
+        while (gate->load() < conns) std::this_thread::yield();
+    }
 
     kmws_tx_batch* tx = lo.tx;
     uint8_t* sring = lo.sring;
@@ -342,7 +359,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             const double tt = now_s();
             iov.assign(v, v + cnt);
             send_all(fd, iov);
-            g_t.writev += now_s() - tt;
+            T.writev += now_s() - tt;
             return 0;
         });
         for (int g0 = 0; g0 < kFrames; g0 += kGroup) {
@@ -358,16 +375,16 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 std::memcpy(h.maskey, &key, 4);
                 if (txl.send(conn, h, e.plain.data() + (size_t)(g0 + j) * kLen, kLen) < 0) std::exit(7);
             }
-            const double tt = now_s(), w0 = g_t.writev;
+            const double tt = now_s(), w0 = T.writev;
             std::vector<kmws::TxLoop::Task> now;
             now.swap(ctasks);
             for (auto& t : now) t();
             if (txl.lastResult() < 0 || conn->lastResult() < 0) std::exit(7);
-            g_t.tx_flush += now_s() - tt - (g_t.writev - w0);
+            T.tx_flush += now_s() - tt - (T.writev - w0);
         }
-        const double tt = now_s(), w0 = g_t.writev;
+        const double tt = now_s(), w0 = T.writev;
         if (txl.close(conn) < 0) std::exit(7);  // the last generations: masked and written
-        g_t.tx_flush += now_s() - tt - (g_t.writev - w0);
+        T.tx_flush += now_s() - tt - (T.writev - w0);
     }
     for (int g0 = 0; g0 < kFrames && !adapter; g0 += kGroup) {
         const int ng = std::min(kGroup, kFrames - g0);
@@ -415,7 +432,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         } else if (gpu && !g_sync && kmws_tx_batch_flush(tx) != ng) {
             std::exit(7);
         }
-        g_t.tx_flush += now_s() - tt;
+        T.tx_flush += now_s() - tt;
         iov.clear();
         for (int j = 0; j < ng; ++j) {
             iov.push_back(iovec{hdrs[j].data(), (size_t)hlen[j]});
@@ -423,12 +440,14 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         }
         tt = now_s();
         send_all(fd, iov);
-        g_t.writev += now_s() - tt;
+        T.writev += now_s() - tt;
     }
-    g_t.client = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    T.client = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     server.join();
     close(fd);
     close(ls);
+    T.t0 = std::chrono::duration<double>(t0.time_since_epoch()).count();
+    T.t_end = std::chrono::duration<double>(t_end.time_since_epoch()).count();
     return std::chrono::duration<double>(t_end - t0).count();
 }
 
@@ -444,6 +463,7 @@ int main(int argc, char** argv)
     g_submitpoll = argc > 5 && std::string(argv[5]) == "submitpoll";
     if (argc > 5 && std::string(argv[5]) == "inflight2") g_inflight = 2;
     if (argc > 5 && std::string(argv[5]) == "ring16m") g_tx_ring = (size_t)16 << 20;
+    const int conns = argc > 6 ? std::max(1, std::min(8, std::atoi(argv[6]))) : 1;
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     const bool adapter = mode == "adapter";
     g_sync = mode == "sync";
@@ -452,13 +472,19 @@ int main(int argc, char** argv)
         std::printf("{\"mode\": \"gpu\", \"error\": \"no gfx950 device\"}\n");
         return 1;
     }
-    Expect e;
-    e.plain.resize((size_t)kFrames * kLen);
-    for (size_t i = 0; i < e.plain.size(); ++i) e.plain[i] = (uint8_t)(0x20 + splitmix(i) % 95);
+    std::vector<uint8_t> plain((size_t)kFrames * kLen);
+    for (size_t i = 0; i < plain.size(); ++i) plain[i] = (uint8_t)(0x20 + splitmix(i) % 95);
     std::vector<uint32_t> keys(kFrames);
     for (int i = 0; i < kFrames; ++i) keys[i] = (uint32_t)splitmix(0x6b756d61ull + i);
-    LoopObjs lo;
-    if (gpu) {
+    // one client and one server loop thread per connection, each pair with its own
+    // long-lived loop objects (kuma runs several loop threads, each with its connections)
+    std::vector<Expect> es(conns);
+    std::vector<LoopObjs> los(conns);
+    std::vector<Times> ts(conns);
+    for (int c = 0; c < conns; ++c) {
+        es[c].plain = plain;
+        if (!gpu) continue;
+        LoopObjs& lo = los[c];
         lo.rx = kmws_rx_batch_create(0);
         lo.rring = static_cast<uint8_t*>(kmws_host_alloc(kRing, 0));
         lo.tx = kmws_tx_batch_create(0);
@@ -474,30 +500,58 @@ int main(int argc, char** argv)
             return 3;
         }
     }
-    double best = 1e9;
+    double best = 1e9, best_cpu = 0, best_wall = 0;
     bool ok = true;
-    for (int r = 0; r < reps + 1; ++r) {  // first connection warms up (staging growth, GPU context)
-        const double t = run_once(gpu, adapter, e, keys, lo);
-        ok = ok && e.got.load() == kFrames && e.bad.load() == 0;
-        if (r) best = std::min(best, t);
+    for (int r = 0; r < reps + 1; ++r) {  // first round of connections warms up (staging growth, GPU context)
+        double t = 0;
+        const double c0 = cpu_s(), w0 = now_s();
+        if (conns == 1) {
+            t = run_once(gpu, adapter, es[0], keys, los[0], ts[0]);
+        } else {
+            std::atomic<int> gate{0};
+            std::vector<std::thread> th;
+            for (int c = 0; c < conns; ++c)
+                th.emplace_back([&, c] {
+                    if (g_noresident) kmws_resident_enable(0, 0);  // this client thread
+                    run_once(gpu, adapter, es[c], keys, los[c], ts[c], &gate, conns);
+                });
+            for (auto& x : th) x.join();
+            double t0 = 1e30, t1 = 0;  // the first send of any connection to the last frame of any
+            for (const Times& x : ts) {
+                t0 = std::min(t0, x.t0);
+                t1 = std::max(t1, x.t_end);
+            }
+            t = t1 - t0;
+        }
+        for (const Expect& x : es) ok = ok && x.got.load() == kFrames && x.bad.load() == 0;
+        if (r && t < best) {
+            best = t;
+            best_cpu = cpu_s() - c0;  // the whole rep: connection set-up and thread start included
+            best_wall = now_s() - w0;
+        }
     }
     if (gpu) {
-        delete lo.rxloop;
-        delete lo.txloop;
-        kmws_rx_batch_destroy(lo.rx);
-        kmws_tx_batch_destroy(lo.tx);
-        kmws_host_free(lo.rring);
-        kmws_host_free(lo.sring);
+        for (LoopObjs& lo : los) {
+            delete lo.rxloop;
+            delete lo.txloop;
+            kmws_rx_batch_destroy(lo.rx);
+            kmws_tx_batch_destroy(lo.tx);
+            kmws_host_free(lo.rring);
+            kmws_host_free(lo.sring);
+        }
     }
-    const double bytes = (double)kFrames * kLen;
-    std::printf("{\"mode\": \"%s\", \"frames\": %d, \"frame_len\": %zu, \"frames_per_send_iteration\": %d, "
+    const Times& g = ts[0];
+    const double bytes = (double)kFrames * kLen * conns;
+    std::printf("{\"mode\": \"%s\", \"connections\": %d, \"frames\": %d, \"frame_len\": %zu, \"frames_per_send_iteration\": %d, "
                 "\"rx_flush_bytes\": %zu, \"best_of\": %d, \"GiB_s\": %.3f, \"us_per_frame\": %.3f, "
+                "\"cpu_cores_busy\": %.2f, \"cpu_ms_per_MiB\": %.4f, "
                 "\"verified\": %s, \"breakdown_ms_last_connection\": {\"client_total\": %.3f, "
                 "\"tx_flush\": %.3f, \"writev\": %.3f, \"server_recv\": %.3f, \"rx_feed\": %.3f, "
                 "\"rx_flush\": %.3f, \"rx_task_max\": %.3f, \"rx_wrap_flush\": %.3f, \"rx_wraps\": %d, \"rx_inflight_max\": %d}}\n",
-                mode.c_str(), kFrames, kLen, kGroup, kFlushBytes, reps, bytes / best / (1u << 30),
-                best / kFrames * 1e6, ok ? "true" : "false", g_t.client * 1e3, g_t.tx_flush * 1e3, g_t.writev * 1e3,
-                g_t.recv * 1e3, g_t.rx_feed * 1e3, g_t.rx_flush * 1e3, g_t.rx_task_max * 1e3, g_t.rx_wrap * 1e3,
-                g_t.rx_wraps, g_t.rx_inflight_max);
+                mode.c_str(), conns, kFrames, kLen, kGroup, kFlushBytes, reps, bytes / best / (1u << 30),
+                best / (kFrames * conns) * 1e6, best_wall > 0 ? best_cpu / best_wall : 0.0,
+                best_cpu * 1e3 / (bytes / (1 << 20)), ok ? "true" : "false", g.client * 1e3, g.tx_flush * 1e3, g.writev * 1e3,
+                g.recv * 1e3, g.rx_feed * 1e3, g.rx_flush * 1e3, g.rx_task_max * 1e3, g.rx_wrap * 1e3,
+                g.rx_wraps, g.rx_inflight_max);
     return ok ? 0 : 1;
 }

@@ -22,13 +22,18 @@
 //           (WebSocketImpl.cpp:388), 1 KiB, 4 KiB and 64 KiB payloads in a
 //           pageable buffer: the oracle's byte loop vs
 //           kmws::ws::WSHandler::handleDataMask (resident worker / launch).
+//   mask_sync_threads  handleDataMask of 4 KiB on T = 1, 2, 4, 8, 16 threads at
+//           once (a slot each), `calls` calls per thread: the per-call median
+//           and 99th percentile over every thread, and the aggregate calls/s;
+//           with "idle": one thread masks while T - 1 others hold slots of the
+//           grid without jobs (what the other slots' polling costs one job).
 //
 // Only the codec call is timed (the copy of the next read into the buffer,
 // standing in for recv, is not); best of `reps` passes.  Every decoded payload
 // and every masked buffer is checked.  One JSON line per case.  Test
 // infrastructure (links the oracle): tests/test_abi_build.py, tools/bench_configs.py.
 //
-// usage: sync_cfg1 [reps]
+// usage: sync_cfg1 [reps] [only: mask_threads]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -158,6 +163,64 @@ double time_threads(int T, int passes, const std::vector<uint8_t>& wire,
     return secs(Clock::now() - t0);
 }
 
+// T threads masking `len` bytes per call with the drop-in's static handleDataMask
+// (each thread its slot); active = how many of them mask (the others only hold a
+// slot: one call, then they wait at the end).  Prints one JSON line; false on a
+// wrong result.
+bool mask_threads(int T, int active, size_t len, int calls)
+{
+    std::atomic<int> ready{0}, done{0};
+    std::atomic<bool> go{false};
+    std::vector<std::vector<double>> lat(T);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::vector<uint8_t> src(len), buf(len);
+            for (size_t i = 0; i < len; ++i) src[i] = (uint8_t)splitmix(len * 131 + t * 7 + i);
+            const uint8_t key[4] = {(uint8_t)(0x37 + t), 0xfa, 0x21, 0x3d};
+            std::vector<uint8_t> want = src;
+            orc_mask(key, want.data(), len, 0);
+            buf = src;
+            if (kmws::ws::WSHandler::handleDataMask(key, buf.data(), len) != KMWS_OK || buf != want) bad.fetch_add(1);
+            buf = src;
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            if (t < active) {
+                lat[t].reserve(calls);
+                for (int i = 0; i < calls; ++i) {
+                    const auto t0 = Clock::now();
+                    kmws::ws::WSHandler::handleDataMask(key, buf.data(), len);
+                    lat[t].push_back(secs(Clock::now() - t0));
+                }
+                if (buf != (calls % 2 ? want : src)) bad.fetch_add(1);
+                done.fetch_add(1);
+            } else {  // holds its slot idle until the maskers are done
+                while (done.load() < active) std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+        });
+    while (ready.load() < T) std::this_thread::yield();
+    uint64_t jobs0 = 0, jobs1 = 0, inc0 = 0, inc1 = 0;
+    kmws_resident_info(0, &jobs0, &inc0, nullptr);
+    const auto t0 = Clock::now();
+    go.store(true, std::memory_order_release);
+    while (done.load() < active) std::this_thread::yield();
+    kmws_resident_info(0, &jobs1, &inc1, nullptr);
+    const double wall = secs(Clock::now() - t0);
+    for (auto& x : th) x.join();
+    std::vector<double> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    std::printf("{\"case\": \"mask_sync_threads\", \"codec\": \"kmws_resident\", \"threads\": %d, \"masking\": %d, "
+                "\"len\": %zu, \"calls_per_thread\": %d, \"us_median\": %.3f, \"us_p99\": %.3f, "
+                "\"calls_per_s\": %.0f, \"resident_jobs\": %llu, \"incarnations\": %llu, \"verified\": %s}\n",
+                T, active, len, calls, all[all.size() / 2] * 1e6, all[all.size() * 99 / 100] * 1e6,
+                (double)active * calls / wall, (unsigned long long)(jobs1 - jobs0), (unsigned long long)(inc1 - inc0),
+                bad.load() == 0 ? "true" : "false");
+    std::fflush(stdout);
+    return bad.load() == 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -166,6 +229,13 @@ int main(int argc, char** argv)
     if (kmws_device_count() < 1) {
         std::printf("{\"error\": \"no gfx950 device\"}\n");
         return 1;
+    }
+    if (argc > 2 && std::string(argv[2]) == "mask_threads") {
+        bool ok = true;
+        for (int T : {1, 2, 4, 8, 16}) ok &= mask_threads(T, T, 4096, 2000);
+        for (int T : {2, 4, 8, 16}) ok &= mask_threads(T, 1, 4096, 2000);
+        for (int T : {1, 4, 16}) ok &= mask_threads(T, T, 65536, 500);
+        return ok ? 0 : 1;
     }
     // the cfg1 wire: n x (81 fe 10 00 <key>) + payload ^ key
     std::vector<uint8_t> plain((size_t)kFrames * kLen), wire;

@@ -102,6 +102,16 @@ def test_loopback_cfg1_cpu_codec(tmp_path):
     assert d["verified"] and d["frames"] == 1000
 
 
+def test_loopback_cfg1_cpu_codec_three_connections(tmp_path):
+    """Three client / server loop-thread pairs at once, 1,000 frames each."""
+    import json
+    r = subprocess.run([str(_build_loopback(tmp_path)), "cpu", "2", "16", "0", "0", "3"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["verified"] and d["connections"] == 3
+
+
 @pytest.mark.gpu
 def test_loopback_cfg1_gpu_codec(tmp_path):
     """1,000 masked frames client -> server over loopback through kmws_tx_batch and
@@ -138,6 +148,20 @@ def test_loopback_cfg1_adapter_batched(tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["verified"] and d["frames"] == 1000 and d["mode"] == "adapter"
+
+
+@pytest.mark.gpu
+def test_loopback_cfg1_four_connections_share_the_resident_worker(tmp_path):
+    """Four connections at once, each with its own client and server loop thread
+    (eight threads holding resident slots): the adapter, the loop-batched mode and
+    the synchronous member swap deliver every payload of every connection intact."""
+    import json
+    exe = _build_loopback(tmp_path)
+    for mode in ("adapter", "gpu", "sync"):
+        r = subprocess.run([str(exe), mode, "2", "16", "0", "0", "4"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["verified"] and d["connections"] == 4 and d["mode"] == mode
 
 
 def _build_sync(tmp_path):

@@ -428,6 +428,54 @@ def test_resident_lease_relaunches_a_busy_worker():
     assert after["launches"] - before["launches"] >= 10, (n, before, after)
 
 
+def test_decoders_per_connection_borrow_pooled_staging():
+    """kuma creates a WSHandler per connection.  300 short-lived decoders, each
+    fed one masked frame, borrow the process's pooled pinned stages (no stream
+    or pinned allocation per connection): every payload exact and the mean
+    connection well under a stream creation's milliseconds.  A callback that
+    feeds a second decoder (a relay) borrows a second stage: both exact."""
+    import time
+    rng = random.Random(41)
+    payload = bytes(rng.randrange(256) for _ in range(1024))
+    key = b"\x11\x22\x33\x44"
+    wire = orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=1, maskey=key, length=len(payload))) + \
+        orc.mask_bytes(key, payload)
+    got = []
+
+    def one():
+        h = kmws.WSHandler(kmws.SERVER)
+        h.setFrameCallback(lambda hdr, data: got.append(data))
+        assert h.handleData(bytearray(wire)) == 0
+        del h
+
+    one()
+    got.clear()
+    t0 = time.perf_counter()
+    for _ in range(300):
+        one()
+    dt = (time.perf_counter() - t0) / 300
+    print(f"\nper connection (create, one masked 1 KiB frame, destroy): {dt * 1e6:.1f} us")
+    assert got == [payload] * 300
+    assert dt < 5e-4, dt
+    # nested: decoder A's callback feeds decoder B while A's staged payload is delivered
+    key_b = b"\xa0\xb1\xc2\xd3"
+    inner = orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=1, maskey=key_b, length=len(payload))) + \
+        orc.mask_bytes(key_b, payload[::-1])
+    outer = orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=1, maskey=key, length=len(inner))) + \
+        orc.mask_bytes(key, inner)
+    b = kmws.WSHandler(kmws.SERVER)
+    seen = []
+    b.setFrameCallback(lambda hdr, data: seen.append(("b", data)))
+    a = kmws.WSHandler(kmws.SERVER)
+
+    def relay(hdr, data):
+        seen.append(("a", data))
+        assert b.handleData(bytearray(data)) == 0
+    a.setFrameCallback(relay)
+    assert a.handleData(bytearray(outer + outer)) == 0
+    assert seen == [("a", inner), ("b", payload[::-1])] * 2
+
+
 def test_resident_worker_slot_per_thread():
     """Four threads masking concurrently each hold their own mailbox slot of
     the device's resident grid (no lock between them): distinct slots, every

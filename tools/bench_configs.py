@@ -106,6 +106,14 @@ def loopback(reps: int):
                 for x in got:
                     x["variant"] = extra[1] if extra else ""
                 rows += got
+        for conns in ("2", "4", "8"):  # loop-thread pairs at once, 64 KiB per send iteration
+            for mode in ("cpu", "sync", "gpu", "adapter"):
+                r = subprocess.run([exe, mode, str(reps), "16", "0", "0", conns], capture_output=True, text=True,
+                                   timeout=300)
+                got = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
+                for x in got:
+                    x["variant"] = "conns" + conns
+                rows += got
     out = {"config": "loopback_cfg1", "rows": rows}
     for x in rows:
         out.setdefault("GiB_s", {}).setdefault(str(x.get("frames_per_send_iteration")), {})[
