@@ -152,12 +152,30 @@ namespace {
 // pinned area made once: a decoder per connection (kuma's WSHandler) would
 // otherwise create a stream (milliseconds) and 1 MiB of pinned memory per
 // connection, and a new loop thread its own.  Never freed (pinned memory must
-// not be released after the HIP runtime's teardown at process exit).
+// not be released after the HIP runtime's teardown at process exit).  Each
+// thread keeps the stage it gave back last in front of the pool, so its calls
+// take no lock (16 threads masking at once contended on the pool's mutex); a
+// nested call, or a call for another device, goes to the pool, and a thread's
+// kept stage returns to it when the thread exits.
+class StagePool;
+StagePool& stage_pool();
+
+struct HotStage {  // the calling thread's kept stage
+    PinnedStage* s = nullptr;
+    ~HotStage();
+};
+thread_local HotStage t_hot;
+
 class StagePool {
 public:
     PinnedStage* take(int device, kmws_status* st)
     {
         *st = KMWS_OK;
+        if (t_hot.s && t_hot.s->device() == device) {
+            PinnedStage* s = t_hot.s;
+            t_hot.s = nullptr;
+            return s;
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (size_t i = free_.size(); i-- > 0;)  // the most recently used first (warm in cache)
@@ -180,9 +198,13 @@ public:
         }
         return s;
     }
-    void give(PinnedStage* s)
+    void give(PinnedStage* s, bool keep = true)
     {
         s->clear();
+        if (keep && !t_hot.s) {
+            t_hot.s = s;
+            return;
+        }
         std::lock_guard<std::mutex> lk(mu_);
         free_.push_back(s);
     }
@@ -196,6 +218,11 @@ StagePool& stage_pool()
 {
     static StagePool* p = new StagePool();
     return *p;
+}
+
+HotStage::~HotStage()
+{
+    if (s) stage_pool().give(s, false);
 }
 
 // A stage borrowed for the scope of one call (taken at first use).

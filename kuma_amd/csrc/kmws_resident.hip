@@ -461,9 +461,9 @@ public:
         for (uint32_t i = 0; i < n; ++i)
             if ((d[i].addr >> 48) != 0 || d[i].len > kLenMask) return KMWS_ERR_NOT_SUPPORTED;
         ResSlot& sl = mb_->slot[b];
-        const uint64_t prev = seq_[b];
+        const uint64_t prev = hs_[b].seq;
         uint64_t cur = ld_acq(&inc_);
-        if (cancelled_[b] != prev && !all_done(sl, prev, parts_[b])) {  // busy: the caller launches
+        if (hs_[b].cancelled != prev && !all_done(sl, prev, hs_[b].parts)) {  // busy: the caller launches
             // (a job a previous holder left posted: a grid that left is relaunched for it)
             if (cur && ld_acq(&mb_->exited) == cur) (void)relaunch(cur);
             return KMWS_ERR_NOT_SUPPORTED;
@@ -484,9 +484,9 @@ public:
             __atomic_store_n(q, x.addr, __ATOMIC_RELAXED);
             __atomic_store_n(q + 1, (uint64_t)x.len | (uint64_t)x.key << 32, __ATOMIC_RELAXED);
         }
-        seq_[b] = s;
-        parts_[b] = parts;
-        __atomic_fetch_add(&jobs_, 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
+        hs_[b].seq = s;
+        hs_[b].parts = parts;
+        __atomic_store_n(&hs_[b].jobs, hs_[b].jobs + 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
         __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | (uint64_t)(parts - 1) << kPartShift | kClaimedBit,
                          __ATOMIC_RELEASE);
         *job = s;
@@ -530,7 +530,7 @@ public:
                     continue;
                 }
                 orphan = Clock::time_point{};
-            } else if (part_left(sl, s, parts_[b], cur)) {  // a part's workgroup left, others run on
+            } else if (part_left(sl, s, hs_[b].parts, cur)) {  // a part's workgroup left, others run on
                 if (finished(b, s)) return KMWS_OK;
                 const auto now = Clock::now();
                 if (orphan == Clock::time_point{}) orphan = now;
@@ -543,7 +543,12 @@ public:
         }
     }
 
-    uint64_t jobs() const { return ld_acq(&jobs_); }
+    uint64_t jobs() const
+    {
+        uint64_t n = 0;
+        for (const SlotHost& h : hs_) n += __atomic_load_n(&h.jobs, __ATOMIC_RELAXED);
+        return n;
+    }
     uint64_t launches() const { return ld_acq(&inc_); }
     uint64_t timeouts() const { return ld_acq(&timeouts_); }
     uint64_t withdrawn() const { return ld_acq(&withdrawn_); }
@@ -564,7 +569,7 @@ private:
     }
     // Job s of slot b finished -- or the slot has moved on (a later job is
     // posted only once s was finished or withdrawn, by s's own waiter).
-    bool finished(int b, uint64_t s) const { return seq_[b] != s || all_done(mb_->slot[b], s, parts_[b]); }
+    bool finished(int b, uint64_t s) const { return hs_[b].seq != s || all_done(mb_->slot[b], s, hs_[b].parts); }
     // Has the workgroup of an unfinished part of job s left grid `cur`?
     static bool part_left(const ResSlot& sl, uint64_t s, uint32_t parts, uint64_t cur)
     {
@@ -584,16 +589,16 @@ private:
     {
         ResSlot& sl = mb_->slot[b];
         std::lock_guard<std::mutex> lk(launch_mu_);
-        if (ld_acq(&inc_) != cur || seq_[b] != s) return false;
+        if (ld_acq(&inc_) != cur || hs_[b].seq != s) return false;
         const bool all_left = ld_acq(&mb_->exited) == cur;
-        for (uint32_t j = 0; j < parts_[b]; ++j) {
+        for (uint32_t j = 0; j < hs_[b].parts; ++j) {
             if (job_done(ld_acq(&sl.done[j]), s)) return false;
             if (!all_left && ld_acq(&sl.gone[j]) != cur) return false;
         }
         __atomic_store_n(&sl.word, (ld_acq(&sl.word) | kCancelBit) & ~kQuitBit, __ATOMIC_RELEASE);
-        cancelled_[b] = s;
+        hs_[b].cancelled = s;
         __atomic_fetch_add(&withdrawn_, 1, __ATOMIC_RELAXED);
-        __atomic_fetch_sub(&jobs_, 1, __ATOMIC_RELAXED);
+        __atomic_store_n(&hs_[b].jobs, hs_[b].jobs - 1, __ATOMIC_RELAXED);
         return true;
     }
 
@@ -602,7 +607,7 @@ private:
     kmws_status timed_out(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
-        const uint32_t parts = parts_[b];
+        const uint32_t parts = hs_[b].parts;
         __atomic_fetch_add(&timeouts_, 1, __ATOMIC_RELAXED);
         __atomic_fetch_or(&sl.word, kQuitBit, __ATOMIC_RELEASE);
         const auto t0 = Clock::now();
@@ -724,10 +729,19 @@ private:
     uint64_t inc_ = 0;  // latest incarnation launched
     uint32_t nslots_ = 0;     // slots the latest incarnation serves
     uint64_t exit_base_ = 0;  // workgroups launched in all incarnations so far
-    uint64_t seq_[kResSlots] = {};        // last job number posted per slot (by its holder)
-    uint32_t parts_[kResSlots] = {};      // its parts
-    uint64_t cancelled_[kResSlots] = {};  // the last job withdrawn per slot
-    uint64_t jobs_ = 0, timeouts_ = 0, withdrawn_ = 0;
+    // Per slot, written by its holder thread (a withdraw by the holder too,
+    // under launch_mu_), each on a cache line of its own: a thread spinning on
+    // its job reads its own line only, and another thread's post does not
+    // invalidate it (16 threads shared three arrays and one job counter before).
+    struct alignas(64) SlotHost {
+        uint64_t seq = 0;        // last job number posted
+        uint64_t cancelled = 0;  // the last job withdrawn
+        uint64_t jobs = 0;       // jobs posted and not withdrawn (summed by jobs())
+        uint32_t parts = 0;      // parts of job `seq`
+    };
+    SlotHost hs_[kResSlots];
+    alignas(64) uint64_t timeouts_ = 0;
+    uint64_t withdrawn_ = 0;
 };
 
 // Every worker of the process (for the exit handler); never freed.
