@@ -122,7 +122,14 @@ public:
     kmws_rx_batch* batch() const { return batch_; }
     // (Re)binds the loop's post function (e.g. when the loop object is created
     // before its event loop runs).
-    void setPoster(Poster post) { post_ = std::move(post); }
+    // A new poster holds none of this loop's tasks: the next arm() posts again
+    // (a task left with the old one never ran, or runs as a harmless extra pass).
+    void setPoster(Poster post)
+    {
+        post_ = std::move(post);
+        armed_ = false;
+        if (pending() > 0 || inflight() > 0) arm();
+    }
 
     // Pinned receive ring the loop reads sockets into (kmws_host_alloc): payloads
     // lying in it are unmasked there, without copies.  Ring bytes of a frame
@@ -249,7 +256,14 @@ public:
     }
 
     bool valid() const { return batch_ != nullptr && ring_ != nullptr; }
-    void setPoster(Poster post) { post_ = std::move(post); }
+    // A new poster holds none of this loop's tasks: the next arm() posts again
+    // (a task left with the old one never ran, or runs as a harmless extra pass).
+    void setPoster(Poster post)
+    {
+        post_ = std::move(post);
+        armed_ = false;
+        if (pending() > 0 || inflight() > 0) arm();
+    }
 
     // A connection's queue (kuma: per WebSocket::Impl, around ws_conn_->send).
     Conn* open(Writer w)

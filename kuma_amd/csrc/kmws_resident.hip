@@ -166,6 +166,7 @@ struct alignas(256) ResSlot {
 struct ResMailbox {
     ResSlot slot[kResSlots];
     alignas(128) uint64_t exited;  // incarnation whose last workgroup has left (device)
+    alignas(128) uint64_t resize;  // (host) incarnations up to this one leave: a slot was claimed outside them
     alignas(128) uint64_t pad3;
 };
 // Device memory, shared by the grid's workgroups.  Counters and marks are
@@ -222,12 +223,22 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
             bool polled_full = false;
             for (uint32_t it = 0;; ++it) {
                 const uint64_t now = wall_clock64();
-                bool leave = (uint64_t)(now - born) > lease_ticks;  // a posted job waits for the relaunch
-                if (!leave && (it & 3u) == 0) leave = ld_agent(&ctl->closing) >= inc;
-                if (leave) break;
                 const uint64_t* a = full ? pw : pw0;
                 v0 = ld_sys(a);
                 v1 = ld_sys(a + 1);
+                // every 4th poll, with the word's loads in flight: is the grid
+                // leaving (idle) or asked to (a thread claimed a slot it does not
+                // serve: the relaunch serves it)?  A posted job waits for the
+                // relaunch, as it does at the lease.
+                uint64_t closing = 0, resize = 0;
+                if ((it & 3u) == 0) {
+                    closing = ld_agent(&ctl->closing);
+                    resize = ld_sys(&mb->resize);
+                }
+                if ((uint64_t)(now - born) > lease_ticks || closing >= inc || resize >= inc) {
+                    cmd = 0;
+                    break;
+                }
                 polled_full = full;
                 const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0) |
                                    (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32;
@@ -411,6 +422,10 @@ public:
             if (__atomic_compare_exchange_n(&claimed_, &m, m | (1u << b), false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
                 // the workgroup polls the descriptors from now on (no job: same number)
                 __atomic_fetch_or(&mb_->slot[b].word, kClaimedBit, __ATOMIC_RELEASE);
+                // a running incarnation without this slot's workgroups is asked
+                // to leave; the next job relaunches a grid that serves it
+                const uint64_t cur = ld_acq(&inc_);
+                if (cur && (uint32_t)b >= ld_acq(&nslots_)) request_resize(cur);
                 return b;
             }
         }
@@ -471,8 +486,12 @@ public:
         if (cur == 0 || ld_acq(&mb_->exited) == cur) cur = relaunch(cur);
         if (cur == 0) return KMWS_ERR_NOT_SUPPORTED;
         // a slot claimed after the running incarnation was launched has no
-        // workgroups in it: launch until the next incarnation (<= the lease)
-        if ((uint32_t)b >= ld_acq(&nslots_)) return KMWS_ERR_NOT_SUPPORTED;
+        // workgroups in it: that incarnation was asked to leave (claim); launch
+        // until it has, and the next post relaunches
+        if ((uint32_t)b >= ld_acq(&nslots_)) {
+            request_resize(cur);
+            return KMWS_ERR_NOT_SUPPORTED;
+        }
         const uint64_t s = (prev + 1) & kJobMask;
         uint64_t words = 0;
         for (uint32_t i = 0; i < n; ++i) words += hull_words(d[i].addr, d[i].len);
@@ -687,6 +706,14 @@ private:
         static std::once_flag once;
         std::call_once(once, [] { std::atexit(quit_all_workers); });
         return KMWS_OK;
+    }
+
+    // Incarnations up to `cur` leave at their next few polls (monotonic).
+    void request_resize(uint64_t cur)
+    {
+        uint64_t r = ld_acq(&mb_->resize);
+        while (r < cur && !__atomic_compare_exchange_n(&mb_->resize, &r, cur, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+        }
     }
 
     // Launches the next incarnation once `seen` (0: none yet) has left

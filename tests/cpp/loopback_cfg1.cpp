@@ -104,18 +104,40 @@ double cpu_s()  // CPU time of every thread of the process so far (user + system
     return (double)u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6;
 }
 
+double thread_cpu_s()
+{
+    rusage u{};
+    getrusage(RUSAGE_THREAD, &u);
+    return (double)u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6;
+}
+
 double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-struct Times {  // seconds spent per step in the last connection (breakdown)
-    double tx_flush = 0, writev = 0, rx_feed = 0, rx_flush = 0, recv = 0, client = 0;
+// Seconds spent per step of one connection (breakdown).  The client's and the
+// server's fields are on cache lines of their own, and so is each connection's
+// record: a server spinning on recv updates its fields at every pass, and
+// fields shared with a client or another connection's record made those
+// threads ping-pong the line (it cost the other threads milliseconds per
+// connection at 8 connections).
+struct alignas(64) Times {
+    // client thread
+    double tx_flush = 0, writev = 0, client = 0, t0 = 0;  // t0: this connection's first send (steady clock)
+    double sends = 0;          // adapter client: inside TxLoop::send
+    double client_cpu = 0;     // the client thread's own CPU time
+    long client_nivcsw = 0;    // its involuntary context switches
+    int client_slot = -1;      // its slot of the resident grid (-1: none)
+    // server thread
+    alignas(64) double rx_feed = 0, rx_flush = 0, recv = 0;
     double rx_task_max = 0, rx_wrap = 0;  // adapter: the longest posted rx task; flushes at ring wraps
     int rx_wraps = 0, rx_inflight_max = 0;
-    double t0 = 0, t_end = 0;  // this connection's first send and last delivered frame (steady clock)
-} g_t;
+    double t_end = 0;        // the last delivered frame (steady clock)
+    double server_cpu = 0;   // the server thread's own CPU time
+    int server_slot = -1;
+};
 
-struct Expect {
+struct alignas(64) Expect {  // one connection's (a line of its own: the server thread updates it per frame)
     std::vector<uint8_t> plain;  // kFrames * kLen
     std::atomic<int> got{0};
     std::atomic<int> bad{0};
@@ -206,6 +228,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         int one = 1;
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
         ready = true;
+        const double sc0 = thread_cpu_s();
         if (g_sync) {
             kmws::ws::WSHandler h;  // per connection; no RxLoop: one synchronous GPU job per read
             h.setMode(kmws::ws::WSMode::SERVER);
@@ -325,6 +348,8 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             orc_decoder_destroy(d);
         }
         t_end = std::chrono::steady_clock::now();
+        T.server_cpu = thread_cpu_s() - sc0;
+        if (gpu) kmws_resident_counters(0, &T.server_slot, nullptr, nullptr, nullptr);
         close(fd);
     });
 
@@ -349,6 +374,9 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     std::vector<int> hlen(kGroup);
     std::vector<iovec> iov;
     const auto t0 = std::chrono::steady_clock::now();
+    const double cc0 = thread_cpu_s();
+    rusage ru0{};
+    getrusage(RUSAGE_THREAD, &ru0);
     if (adapter) {
         // the client loop thread: its TxLoop (the posted task masks the
         // iteration's sends with one GPU job and writes finished generations)
@@ -373,7 +401,9 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 h.opcode = KMWS_OP_TEXT;
                 h.mask = 1;
                 std::memcpy(h.maskey, &key, 4);
+                const double ts = now_s();
                 if (txl.send(conn, h, e.plain.data() + (size_t)(g0 + j) * kLen, kLen) < 0) std::exit(7);
+                T.sends += now_s() - ts;
             }
             const double tt = now_s(), w0 = T.writev;
             std::vector<kmws::TxLoop::Task> now;
@@ -443,6 +473,17 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         T.writev += now_s() - tt;
     }
     T.client = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    T.client_cpu = thread_cpu_s() - cc0;
+#ifdef KMWS_PROF
+    std::fprintf(stderr, "{\"place_ms\": %.3f, \"copy_ms\": %.3f, \"add_ms\": %.3f, \"push_ms\": %.3f, \"arm_ms\": %.3f, \"waits\": %ld}\n",
+                 kmws::t_txprof.place * 1e3, kmws::t_txprof.copy * 1e3, kmws::t_txprof.add * 1e3, kmws::t_txprof.push * 1e3,
+                 kmws::t_txprof.arm * 1e3, kmws::t_txprof.waits);
+    kmws::t_txprof = kmws::TxProf();
+#endif
+    rusage ru1{};
+    getrusage(RUSAGE_THREAD, &ru1);
+    T.client_nivcsw = ru1.ru_nivcsw - ru0.ru_nivcsw;
+    if (gpu) kmws_resident_counters(0, &T.client_slot, nullptr, nullptr, nullptr);
     server.join();
     close(fd);
     close(ls);
@@ -501,6 +542,9 @@ int main(int argc, char** argv)
         }
     }
     double best = 1e9, best_cpu = 0, best_wall = 0;
+    // the best rep's connections, ms: [start offset, span, client, tx_flush, writev, server recv, rx_flush,
+    // sends (adapter), client thread CPU, server thread CPU, client involuntary switches, client slot, server slot]
+    std::string spans = "[]";
     bool ok = true;
     for (int r = 0; r < reps + 1; ++r) {  // first round of connections warms up (staging growth, GPU context)
         double t = 0;
@@ -528,6 +572,19 @@ int main(int argc, char** argv)
             best = t;
             best_cpu = cpu_s() - c0;  // the whole rep: connection set-up and thread start included
             best_wall = now_s() - w0;
+            double t0 = 1e30;
+            for (const Times& x : ts) t0 = std::min(t0, x.t0);
+            spans = "[";
+            for (size_t c = 0; c < ts.size(); ++c) {
+                char b[240];
+                std::snprintf(b, sizeof b, "%s[%.3f, %.3f, %.3f, %.3f, %.3f, %.3f, %.3f, %.3f, %.3f, %.3f, %ld, %d, %d]",
+                              c ? ", " : "", (ts[c].t0 - t0) * 1e3, (ts[c].t_end - ts[c].t0) * 1e3, ts[c].client * 1e3,
+                              ts[c].tx_flush * 1e3, ts[c].writev * 1e3, ts[c].recv * 1e3, ts[c].rx_flush * 1e3,
+                              ts[c].sends * 1e3, ts[c].client_cpu * 1e3, ts[c].server_cpu * 1e3, ts[c].client_nivcsw,
+                              ts[c].client_slot, ts[c].server_slot);
+                spans += b;
+            }
+            spans += "]";
         }
     }
     if (gpu) {
@@ -544,13 +601,13 @@ int main(int argc, char** argv)
     const double bytes = (double)kFrames * kLen * conns;
     std::printf("{\"mode\": \"%s\", \"connections\": %d, \"frames\": %d, \"frame_len\": %zu, \"frames_per_send_iteration\": %d, "
                 "\"rx_flush_bytes\": %zu, \"best_of\": %d, \"GiB_s\": %.3f, \"us_per_frame\": %.3f, "
-                "\"cpu_cores_busy\": %.2f, \"cpu_ms_per_MiB\": %.4f, "
+                "\"cpu_cores_busy\": %.2f, \"cpu_ms_per_MiB\": %.4f, \"connection_start_span_ms\": %s, "
                 "\"verified\": %s, \"breakdown_ms_last_connection\": {\"client_total\": %.3f, "
                 "\"tx_flush\": %.3f, \"writev\": %.3f, \"server_recv\": %.3f, \"rx_feed\": %.3f, "
                 "\"rx_flush\": %.3f, \"rx_task_max\": %.3f, \"rx_wrap_flush\": %.3f, \"rx_wraps\": %d, \"rx_inflight_max\": %d}}\n",
                 mode.c_str(), conns, kFrames, kLen, kGroup, kFlushBytes, reps, bytes / best / (1u << 30),
                 best / (kFrames * conns) * 1e6, best_wall > 0 ? best_cpu / best_wall : 0.0,
-                best_cpu * 1e3 / (bytes / (1 << 20)), ok ? "true" : "false", g.client * 1e3, g.tx_flush * 1e3, g.writev * 1e3,
+                best_cpu * 1e3 / (bytes / (1 << 20)), spans.c_str(), ok ? "true" : "false", g.client * 1e3, g.tx_flush * 1e3, g.writev * 1e3,
                 g.recv * 1e3, g.rx_feed * 1e3, g.rx_flush * 1e3, g.rx_task_max * 1e3, g.rx_wrap * 1e3,
                 g.rx_wraps, g.rx_inflight_max);
     return ok ? 0 : 1;

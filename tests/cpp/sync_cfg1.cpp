@@ -172,6 +172,7 @@ bool mask_threads(int T, int active, size_t len, int calls)
     std::atomic<int> ready{0}, done{0};
     std::atomic<bool> go{false};
     std::vector<std::vector<double>> lat(T);
+    std::vector<int> slot(T, -1);
     std::atomic<int> bad{0};
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -194,6 +195,7 @@ bool mask_threads(int T, int active, size_t len, int calls)
                     lat[t].push_back(secs(Clock::now() - t0));
                 }
                 if (buf != (calls % 2 ? want : src)) bad.fetch_add(1);
+                kmws_resident_counters(0, &slot[t], nullptr, nullptr, nullptr);
                 done.fetch_add(1);
             } else {  // holds its slot idle until the maskers are done
                 while (done.load() < active) std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -209,14 +211,24 @@ bool mask_threads(int T, int active, size_t len, int calls)
     const double wall = secs(Clock::now() - t0);
     for (auto& x : th) x.join();
     std::vector<double> all;
+    std::string per = "[";  // [slot, median us] per masking thread
+    for (int t = 0; t < active; ++t) {
+        std::vector<double> v = lat[t];
+        std::sort(v.begin(), v.end());
+        char b[48];
+        std::snprintf(b, sizeof b, "%s[%d, %.2f]", t ? ", " : "", slot[t], v[v.size() / 2] * 1e6);
+        per += b;
+    }
+    per += "]";
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
     std::printf("{\"case\": \"mask_sync_threads\", \"codec\": \"kmws_resident\", \"threads\": %d, \"masking\": %d, "
                 "\"len\": %zu, \"calls_per_thread\": %d, \"us_median\": %.3f, \"us_p99\": %.3f, "
-                "\"calls_per_s\": %.0f, \"resident_jobs\": %llu, \"incarnations\": %llu, \"verified\": %s}\n",
+                "\"calls_per_s\": %.0f, \"resident_jobs\": %llu, \"incarnations\": %llu, \"slot_median_us\": %s, "
+                "\"verified\": %s}\n",
                 T, active, len, calls, all[all.size() / 2] * 1e6, all[all.size() * 99 / 100] * 1e6,
                 (double)active * calls / wall, (unsigned long long)(jobs1 - jobs0), (unsigned long long)(inc1 - inc0),
-                bad.load() == 0 ? "true" : "false");
+                per.c_str(), bad.load() == 0 ? "true" : "false");
     std::fflush(stdout);
     return bad.load() == 0;
 }

@@ -130,13 +130,63 @@ int main(int argc, char** argv)
             if (tx.lastResult() < 0) return 5;
         }
     }
+    // A loop that drops a posted task (it was torn down, or the caller's task
+    // list was discarded), then a new poster: sends are posted again (a stale
+    // armed flag once kept every later send queued until the ring filled).
+    int reposted = 0;
+    {
+        if (tx.flush() < 0) return 8;  // everything written; then the loop's queued tasks run out
+        while (!tasks.empty()) {
+            std::vector<kmws::TxLoop::Task> now;
+            now.swap(tasks);
+            for (auto& t : now) t();
+        }
+        auto frame = [&](uint32_t key, size_t plen, int c) {
+            std::vector<uint8_t> payload(plen);
+            for (auto& b : payload) b = (uint8_t)rnd();
+            kmws_frame_hdr h;
+            std::memset(&h, 0, sizeof h);
+            h.fin = 1;
+            h.opcode = KMWS_OP_BINARY;
+            h.mask = 1;
+            std::memcpy(h.maskey, &key, 4);
+            if (tx.send(conn[c], h, payload.data(), plen) < 0) std::exit(7);
+            orc_hdr o;
+            std::memset(&o, 0, sizeof o);
+            o.fin = 1;
+            o.opcode = KMWS_OP_BINARY;
+            o.mask = 1;
+            std::memcpy(o.maskey, &key, 4);
+            o.length = (uint32_t)plen;
+            uint8_t hb[14];
+            const int hl = orc_encode_header(&o, hb);
+            orc_mask(o.maskey, payload.data(), plen, 0);
+            want[c].append(reinterpret_cast<const char*>(hb), (size_t)hl);
+            want[c].append(reinterpret_cast<const char*>(payload.data()), plen);
+        };
+        frame(0x01020304u, 3000, 0);
+        reposted += tasks.size() == 1;
+        tasks.clear();  // dropped unrun
+        std::vector<kmws::TxLoop::Task> tasks2;
+        tx.setPoster([&tasks2](kmws::TxLoop::Task t) { tasks2.push_back(std::move(t)); });
+        reposted += tasks2.size() == 1;  // something is queued: the new poster gets a task at once
+        frame(0x0a0b0c0du, 5000, 1);
+        reposted += tasks2.size() == 1;  // armed: no second task
+        while (!tasks2.empty()) {
+            std::vector<kmws::TxLoop::Task> now;
+            now.swap(tasks2);
+            for (auto& t : now) t();
+        }
+        reposted += tx.pending() == 0 && tx.inflight() == 0;
+        tx.setPoster([&tasks](kmws::TxLoop::Task t) { tasks.push_back(std::move(t)); });
+    }
     for (int c = 0; c < kConns; ++c)
         if (tx.close(conn[c]) < 0) return 6;
-    bool ok = bad_src == 0;
+    bool ok = bad_src == 0 && reposted == 4;
     for (int c = 0; c < kConns; ++c) ok &= wrote[c] == want[c];
     std::printf("{\"sends\": %d, \"masked\": %d, \"larger_than_ring\": %d, \"iterations\": %d, \"bytes\": [%zu, %zu, %zu], "
-                "\"callers_buffers_changed\": %d, \"exact\": %s}\n",
-                sends, masked_n, heap, runs, wrote[0].size(), wrote[1].size(), wrote[2].size(), bad_src,
+                "\"callers_buffers_changed\": %d, \"reposted_checks\": %d, \"exact\": %s}\n",
+                sends, masked_n, heap, runs, wrote[0].size(), wrote[1].size(), wrote[2].size(), bad_src, reposted,
                 ok ? "true" : "false");
     return ok ? 0 : 1;
 }
