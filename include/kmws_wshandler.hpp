@@ -148,8 +148,13 @@ public:
         });
     }
 
-    // The posted task: submit what the iteration fed, deliver what finished;
-    // re-arms itself while generations are in flight.
+    // The posted task: deliver what finished, then submit what was fed since
+    // -- once the loop's previous generation has finished: one generation in
+    // flight per loop thread, so it always runs on the thread's slot of the
+    // resident grid (a second one posted while the first runs finds the slot
+    // busy and launches; with several in flight the loopback's connections
+    // launched most of their jobs, r05an).  Frames fed meanwhile wait and go
+    // with the next.  Never waits; re-arms itself while anything is queued.
     void runIteration()
     {
         armed_ = false;
@@ -157,8 +162,12 @@ public:
             last_ = kmws_rx_batch_flush(batch_);
             return;
         }
-        const int s = kmws_rx_batch_submit(batch_);
-        last_ = s < 0 ? s : kmws_rx_batch_poll(batch_, 0);
+        int r = kmws_rx_batch_poll(batch_, 0);
+        if (r >= 0 && kmws_rx_batch_inflight(batch_) == 0 && kmws_rx_batch_pending(batch_) > 0) {
+            const int s = kmws_rx_batch_submit(batch_);
+            if (s < 0) r = s;
+        }
+        last_ = r;
         if (kmws_rx_batch_inflight(batch_) > 0 || kmws_rx_batch_pending(batch_) > 0) arm();
     }
 
@@ -185,11 +194,13 @@ private:
 // loop's posted task (kuma: EventLoop::post, kmapi.h:204-210) masks every
 // payload queued in the iteration with ONE GPU job and writes each
 // connection's frames, in send order, as soon as their generation's mask has
-// completed -- the GPU round trip overlaps the next iteration instead of
-// stalling every send.  At most `max_inflight` generations are in flight
-// after a run (1: the task submits iteration k, then writes iteration k - 1,
-// whose masks ran while the loop filled k -- waiting for them only if they
-// have not finished yet).
+// completed -- the GPU round trip overlaps the next iterations instead of
+// stalling every send.  The task never waits: it writes the generations whose
+// masks completed and posts what was sent since as the next generation once
+// fewer than `max_inflight` are in flight (1, the default: one job per loop
+// thread, always on its slot of the resident grid -- a second posted while the
+// first runs finds the slot busy and launches; frames sent meanwhile go with
+// the next generation).
 //
 // Differences from sendWsFrame, observable only to the sender:
 //  * the frame reaches the socket at the iteration's task, not before send()
@@ -369,24 +380,31 @@ public:
         });
     }
 
-    // The posted task: submit the iteration's masks, write every generation
-    // whose masks completed, keep at most max_inflight generations in flight;
-    // re-arms itself while any are.
+    // The posted task: write every generation whose masks completed, then
+    // post what was sent since if fewer than max_inflight generations are in
+    // flight; re-arms itself while anything is queued or in flight.
     void runIteration()
     {
         armed_ = false;
-        int r = submit();
-        if (r >= 0) r = complete(false);
-        while (r >= 0 && (int)inflight_.size() > max_inflight_) r = completeOldest();
+        int r = complete(false);
+        if (r >= 0 && (int)inflight_.size() < max_inflight_) {
+            const int s = submit();
+            if (s < 0) r = s;
+        }
         last_ = r;
-        if (!inflight_.empty()) arm();
+        if (!inflight_.empty() || !cur_.frames.empty()) arm();
     }
 
-    // Everything sent so far masked and written, synchronously.
+    // Everything sent so far masked and written, synchronously (what is in
+    // flight first, so the last generation's job finds the slot free).
     int flush()
     {
-        int r = submit();
-        if (r >= 0) r = complete(true);
+        int r = complete(true);
+        if (r >= 0) {
+            const int s = submit();
+            const int w = s < 0 ? s : complete(true);
+            r = w < 0 ? w : r + w;
+        }
         return last_ = r;
     }
 

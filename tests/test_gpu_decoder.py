@@ -479,10 +479,10 @@ def test_decoders_per_connection_borrow_pooled_staging():
 def test_resident_worker_slot_per_thread():
     """Four threads masking concurrently each hold their own mailbox slot of
     the device's resident grid (no lock between them): distinct slots, every
-    result exact, the jobs on the worker (but those of a slot claimed while
-    the running incarnation did not cover it yet: launched until the next, at
-    most a 1 ms lease later), and the median call stays in the tens of
-    microseconds."""
+    result exact, the jobs on the worker (but the few of a slot claimed while
+    the running incarnation did not cover it: that incarnation is asked to
+    leave at once, and its jobs launch until the relaunch serves it), and the
+    median call stays in the tens of microseconds."""
     import threading
     import time
     rng = random.Random(23)
@@ -514,7 +514,7 @@ def test_resident_worker_slot_per_thread():
     assert all(b == 0 for _, b, _ in res.values()), res
     slots = [s for _, _, s in res.values()]
     assert all(s >= 0 for s in slots) and len(set(slots)) == 4, slots
-    assert 1400 <= after["jobs"] - before["jobs"] <= 1600, (before, after)
+    assert 1560 <= after["jobs"] - before["jobs"] <= 1600, (before, after)
     assert max(m for m, _, _ in res.values()) < 2e-4, res
     # the threads have exited: their slots are free again
     assert kmws.resident_info()["slots_claimed"] <= before["slots_claimed"], (before, kmws.resident_info())
