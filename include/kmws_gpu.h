@@ -48,6 +48,15 @@ typedef int kmws_status;
 #define KMWS_ERR_BUFFER_TOO_LONG  (-18)  /* KMError::BUFFER_TOO_LONG (a send of more than 128 segments) */
 #define KMWS_ERR_NOT_SUPPORTED    (-19)  /* KMError::NOT_SUPPORTED (no gfx950 device) */
 
+/* The resident worker's job limits (kmws_resident.hip): the masked payloads of
+ * one call or one submitted generation, at most KMWS_RESIDENT_MAX_PAYLOADS of
+ * them and KMWS_RESIDENT_MAX_BYTES bytes, run on the calling thread's slot of
+ * the device's resident grid without a kernel launch; larger jobs, and a job
+ * posted while the thread's previous one still runs, launch instead.  The
+ * loop helpers (include/kmws_wshandler.hpp) size their generations to fit. */
+#define KMWS_RESIDENT_MAX_PAYLOADS 128
+#define KMWS_RESIDENT_MAX_BYTES (256u << 10)
+
 /* ---- codec results: WSError (src/ws/wsdefs.h:56-67) ---- */
 enum kmws_ws_error {
     KMWS_WS_NOERR = 0, KMWS_WS_NEED_MORE_DATA = 1, KMWS_WS_HANDSHAKE = 2,
@@ -174,6 +183,7 @@ int            kmws_rx_batch_flush(kmws_rx_batch* b);  /* frames delivered, or n
 int            kmws_rx_batch_submit(kmws_rx_batch* b); /* frames submitted (0: none), or negative status */
 int            kmws_rx_batch_poll(kmws_rx_batch* b, int wait);  /* frames delivered, or negative status */
 int            kmws_rx_batch_pending(const kmws_rx_batch* b);   /* frames fed, not yet submitted */
+uint64_t       kmws_rx_batch_pending_bytes(const kmws_rx_batch* b);  /* their masked payload bytes */
 int            kmws_rx_batch_inflight(const kmws_rx_batch* b);  /* generations submitted, not yet delivered */
 /* Optional pinned receive ring (hipHostMalloc / hipHostRegister, e.g.
  * kmws_host_alloc) that the loop reads sockets into: chunks fed from inside it

@@ -136,7 +136,26 @@ public:
     // must stay unmodified until it was delivered (inflight() == 0 frees all).
     int attachRing(uint8_t* ring, size_t bytes) { return kmws_rx_batch_attach_ring(batch_, ring, bytes); }
 
-    // Called after every deferred feed: posts the iteration's task once.
+    // Called after every deferred feed: posts the iteration's task once, and
+    // keeps generations within the resident worker's job limits -- frames fed
+    // while a generation is in flight wait for it, and once they reach half the
+    // limits (a 64 KiB read adds at most 64 KiB) the one in flight is waited
+    // for (its frames delivered now) and they are submitted at once: a
+    // generation that outgrew the limits would launch, and a loop that had
+    // fallen behind would stay behind (r05ao).
+    void fed()
+    {
+        if (async_ && batch_ &&
+            (kmws_rx_batch_pending(batch_) >= KMWS_RESIDENT_MAX_PAYLOADS / 2 ||
+             kmws_rx_batch_pending_bytes(batch_) >= KMWS_RESIDENT_MAX_BYTES / 2)) {
+            int r = kmws_rx_batch_inflight(batch_) > 0 ? kmws_rx_batch_poll(batch_, 1) : 0;
+            if (r >= 0) r = kmws_rx_batch_submit(batch_);
+            if (r < 0) last_ = r;
+        }
+        arm();
+    }
+
+    // Posts the iteration's task once.
     void arm()
     {
         if (armed_ || !post_) return;
@@ -349,6 +368,17 @@ public:
             c->last_ = c->write_(iov.data(), (int)iov.size());
             return hl;
         }
+        // the generation stays within the resident worker's job limits: one
+        // that would outgrow them is posted first, after the one in flight
+        // (a larger generation would launch, and a loop that fell behind
+        // would stay behind, r05ao)
+        if (masked && !cur_.frames.empty() &&
+            (cur_.nmasked + 1 > KMWS_RESIDENT_MAX_PAYLOADS || cur_.bytes + plen > KMWS_RESIDENT_MAX_BYTES)) {
+            int r = 0;
+            while (r >= 0 && !inflight_.empty()) r = completeOldest();
+            if (r >= 0) r = submit();
+            if (r < 0) return r;
+        }
         uint8_t* p = place(plen, &f);
         if (!p) return KMWS_ERR_FAILED;
         for (size_t i = 0, pos = 0; i < nseg; pos += lens[i], ++i)
@@ -358,6 +388,8 @@ public:
             size_t one = plen;
             f.hlen = kmws_tx_batch_add(batch_, &h, &p, &one, 1, f.hdr);
             cur_.masked = true;
+            ++cur_.nmasked;
+            cur_.bytes += plen;
         } else {
             f.hlen = kmws_encode_header(&h, f.hdr);
         }
@@ -424,6 +456,8 @@ private:
     struct Gen {
         std::vector<Frame> frames;
         bool masked = false;
+        uint32_t nmasked = 0;  // masked payloads (one job descriptor each)
+        uint64_t bytes = 0;    // their bytes
         int64_t ticket = 0;
         size_t ring_used = 0;  // ring bytes (with alignment and wrap waste) freed when written
     };
@@ -655,7 +689,8 @@ private:
         RxLoop* rx = keep->rx;
         const int r = kmws_decoder_feed_deferred(keep->dec, rx->batch(), data, len, &State::on_frame, keep.get());
         if (r == KMWS_WS_NOERR || r == KMWS_WS_NEED_MORE_DATA) {
-            rx->arm();
+            rx->fed();  // may deliver earlier frames (this handler's callback may destroy it)
+            if (!keep->alive) return WSError::DESTROYED;
             keep->last_status = KMWS_OK;
             return static_cast<WSError>(r);
         }

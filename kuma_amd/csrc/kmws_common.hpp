@@ -100,12 +100,12 @@ kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const Pi
 // Resident worker (kmws_resident.hip): host jobs of at most kResMaxDescs
 // payloads and kResMaxBytes bytes go to the calling thread's slot of a grid
 // that stays on the GPU polling pinned memory, instead of a launch per call.
-constexpr int kResMaxDescs = 128;
+constexpr int kResMaxDescs = KMWS_RESIDENT_MAX_PAYLOADS;
 // A job runs on up to four workgroups of its slot (one per 16 KiB of hull
 // words): 256 KiB take ~11 us on the device (tools/zc_probe.hip), a launch of
 // the pieces kernel alone ~20 us.  Synchronous (a flush, a feed, a mask) and
 // asynchronous jobs (an rx / tx batch's submit) alike.
-constexpr uint64_t kResMaxBytes = 256u << 10;
+constexpr uint64_t kResMaxBytes = KMWS_RESIDENT_MAX_BYTES;
 constexpr uint64_t kResMaxBytesAsync = kResMaxBytes;
 struct ResidentJob {
     int device = -1;

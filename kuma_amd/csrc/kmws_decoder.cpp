@@ -105,6 +105,7 @@ struct kmws_rx_batch {
     };
     std::unique_ptr<PinnedStage> stage;  // the generation being fed
     std::vector<Item> items;
+    uint64_t pending_bytes = 0;  // masked payload bytes of `items`
     std::vector<kmws_desc> ring_descs;
     std::deque<Gen> inflight;            // submitted, not yet delivered (submit order)
     std::vector<std::unique_ptr<PinnedStage>> spare;
@@ -870,6 +871,7 @@ int kmws_decoder_feed_deferred(kmws_decoder* dec, kmws_rx_batch* b, const uint8_
         uint32_t key;
         std::memcpy(&key, h.maskey, 4);
         const bool masked = h.mask && h.length;
+        if (masked) b->pending_bytes += h.length;
         if (!reasm && b->ring && payload >= b->ring && payload + h.length <= b->ring + b->ring_bytes) {
             // payload lies in the caller's pinned ring: unmasked there, no copy
             if (masked) b->ring_descs.push_back(kmws_desc{(uint64_t)(payload - b->ring), h.length, key});
@@ -899,6 +901,8 @@ kmws_status kmws_rx_batch_attach_ring(kmws_rx_batch* b, uint8_t* ring, size_t by
 
 int kmws_rx_batch_pending(const kmws_rx_batch* b) { return b ? (int)b->items.size() : 0; }
 
+uint64_t kmws_rx_batch_pending_bytes(const kmws_rx_batch* b) { return b ? b->pending_bytes : 0; }
+
 int kmws_rx_batch_inflight(const kmws_rx_batch* b) { return b ? (int)b->inflight.size() : 0; }
 
 void kmws_rx_batch_discard(kmws_rx_batch* b, const kmws_decoder* dec)
@@ -926,6 +930,7 @@ static int rx_submit(kmws_rx_batch* b, bool sync)
     kmws_status st = sync ? b->stage->run(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv)
                           : b->stage->launch(b->ring, b->ring_bytes, &b->ring_descs, b->ring_dv);
     b->ring_descs.clear();
+    b->pending_bytes = 0;
     if (st != KMWS_OK) {
         // nothing of this generation can be delivered masked: drop it
         b->items.clear();

@@ -39,7 +39,7 @@ EXPORTS = [
     "kmws_unpack_unmask", "kmws_unpack_gather",
     "kmws_pipeline_create", "kmws_pipeline_destroy", "kmws_pipeline_unmask", "kmws_pipeline_set_transfer",
     "kmws_rx_batch_create", "kmws_rx_batch_destroy", "kmws_decoder_feed_deferred", "kmws_rx_batch_flush",
-    "kmws_rx_batch_pending", "kmws_rx_batch_discard", "kmws_mask_host_chain", "kmws_rx_batch_submit",
+    "kmws_rx_batch_pending", "kmws_rx_batch_pending_bytes", "kmws_rx_batch_discard", "kmws_mask_host_chain", "kmws_rx_batch_submit",
     "kmws_rx_batch_poll", "kmws_rx_batch_inflight", "kmws_tx_batch_submit", "kmws_tx_batch_poll",
     "kmws_rx_batch_attach_ring",
     "kmws_tx_batch_create", "kmws_tx_batch_destroy", "kmws_tx_batch_add", "kmws_tx_batch_flush",
@@ -168,6 +168,7 @@ def bind(L: C.CDLL) -> C.CDLL:
         "kmws_rx_batch_flush": (i32, [vp]),
         "kmws_rx_batch_attach_ring": (i32, [vp, vp, sz]),
         "kmws_rx_batch_pending": (i32, [vp]),
+        "kmws_rx_batch_pending_bytes": (C.c_uint64, [vp]),
         "kmws_rx_batch_discard": (None, [vp, vp]),
         "kmws_pipeline_set_transfer": (i32, [vp, i32]),
         "kmws_pipeline_unmask": (i32, [vp, u8p, u64, vp, u32]),
