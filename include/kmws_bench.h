@@ -75,6 +75,11 @@ kmws_status kmws_resident_enable(int device, int on);
 kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, int* running);
 kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_claimed, uint64_t* timeouts,
                                    uint64_t* withdrawn);
+/* Diagnostics: the worker's workgroup exits so far by reason, counts[0..n):
+ * 0 its 1 ms lease ran out, 1 another workgroup found the grid idle, 2 a thread
+ * claimed a slot outside the running incarnation (resize), 3 it found the grid
+ * idle itself, 4 its slot's quit bit.  Reads device memory (synchronous). */
+kmws_status kmws_resident_exit_reasons(int device, uint64_t* counts, int n);
 
 #ifdef __cplusplus
 }

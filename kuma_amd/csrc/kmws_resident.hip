@@ -169,13 +169,18 @@ struct ResMailbox {
     alignas(128) uint64_t resize;  // (host) incarnations up to this one leave: a slot was claimed outside them
     alignas(128) uint64_t pad3;
 };
+// Why a workgroup left: its lease ran out, another workgroup found the grid
+// idle (closing), a thread asked for a resize, it found the grid idle itself,
+// its slot's quit bit.
+constexpr int kResExitReasons = 5;
 // Device memory, shared by the grid's workgroups.  Counters and marks are
 // compared with the incarnation number, so nothing is cleared between launches.
 struct ResCtl {
     uint64_t closing;   // max incarnation that is leaving (idle or lease)
     uint64_t exits;     // workgroups exited, all incarnations (each adds the grid size)
-    uint64_t last_act;  // wall clock of the latest job taken in any slot
+    uint64_t idle;      // workgroups of the running incarnation idle 200 us (or gone on their quit bit)
     uint64_t pad;
+    uint64_t why[kResExitReasons];  // workgroup exits by reason (kmws_resident_exit_reasons)
 };
 
 // Loads of host-written words bypass every cache (and are never scalar loads).
@@ -183,6 +188,10 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// ResCtl lives in uncached device memory (ResidentWorker::init), so a plain
+// load of a word other XCDs update is never served stale from this XCD's L2
+// (a read-modify-write would be coherent too, but 64 workgroups doing one on
+// the same word every fourth poll serialized at the atomic unit).
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -214,8 +223,17 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     // request)
     const uint64_t* pw0 = &sl->word;
     const uint64_t* pw = pw0 + 2 * (t <= kPollDescs ? t : 0);
-    uint64_t last = 0, t_act = born;  // (wave 0) job seen last; latest activity seen
+    // Idle exit without comparing clocks across workgroups: a workgroup whose
+    // slot has had no job for idle_ticks counts itself in ctl->idle (and out
+    // again at the slot's next job, whichever part it is for); the one whose
+    // count completes the grid closes it.  Before, each compared its clock with
+    // a device-wide "last job" time other workgroups wrote, and under load read
+    // it stale or skewed: 16 busy threads' grids closed as idle every ~0.3 ms
+    // (r05as / r05at: 650-1,199 idle decisions in 25 ms; 1.26 M calls/s).
+    uint64_t last = 0, t_act = born;  // (wave 0) job seen last; this slot's latest job
+    bool idle = false;                // (wave 0) counted in ctl->idle
     bool full = part == 0;            // (wave 0) poll the descriptors too
+    uint32_t why = 0;                 // (wave 0) the exit reason (ResCtl::why)
     if (t < 64) last = ld_sys(&sl->done[part]);
     for (;;) {
         if (t < 64) {  // wave 0, uniform control flow
@@ -226,16 +244,17 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 const uint64_t* a = full ? pw : pw0;
                 v0 = ld_sys(a);
                 v1 = ld_sys(a + 1);
-                // every 4th poll, with the word's loads in flight: is the grid
-                // leaving (idle) or asked to (a thread claimed a slot it does not
-                // serve: the relaunch serves it)?  A posted job waits for the
-                // relaunch, as it does at the lease.
+                // with the word's loads in flight: is the grid leaving (idle;
+                // every 4th poll) or asked to (a thread claimed a slot it does
+                // not serve, and the relaunch will; every 16th poll -- every 4th,
+                // 64 workgroups reading that one host word slowed 16 threads'
+                // jobs to 1.4 M/s at an 11 us median, against 2.1 M/s at 6.5 us,
+                // r05av)?  A posted job waits for the relaunch, as at the lease.
                 uint64_t closing = 0, resize = 0;
-                if ((it & 3u) == 0) {
-                    closing = ld_agent(&ctl->closing);
-                    resize = ld_sys(&mb->resize);
-                }
+                if ((it & 3u) == 0) closing = ld_agent(&ctl->closing);
+                if ((it & 15u) == 0) resize = ld_sys(&mb->resize);
                 if ((uint64_t)(now - born) > lease_ticks || closing >= inc || resize >= inc) {
+                    why = closing >= inc ? 1u : resize >= inc ? 2u : 0u;
                     cmd = 0;
                     break;
                 }
@@ -243,25 +262,35 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 const uint64_t w = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v0) |
                                    (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v0 >> 32)) << 32;
                 // (lane 0's job word; each half through uint32_t: readfirstlane is signed)
-                if (w & kQuitBit) break;  // this slot only: the rest of the grid serves on
-                if ((w & kJobMask) != last) {
+                if (w & kQuitBit) {  // this slot only: the rest of the grid serves on
+                    why = 4;
+                    break;
+                }
+                if ((w & kJobMask) != last) {  // a job on this slot: activity, whichever part it is for
+                    t_act = now;
+                    if (idle) {
+                        if (t == 0) __hip_atomic_fetch_sub(&ctl->idle, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        idle = false;
+                    }
                     const uint32_t parts = (uint32_t)(w >> kPartShift & 3u) + 1u;
                     if (part >= parts || (w & kCancelBit)) {
                         last = w & kJobMask;  // not this workgroup's (no done word: nobody waits for it)
                         continue;
                     }
                     cmd = w;
-                    if (t == 0) __hip_atomic_fetch_max(&ctl->last_act, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    t_act = now;
                     break;
                 }
                 const bool claimed = (w & kClaimedBit) != 0;
                 full = part == 0 && claimed;
-                if ((uint64_t)(now - t_act) > idle_ticks) {  // idle here: is every slot idle?
-                    const uint64_t g = ld_agent(&ctl->last_act);
-                    if ((int64_t)(g - t_act) > 0) t_act = g;
-                    if ((uint64_t)(now - t_act) > idle_ticks) {
+                if (!idle && (uint64_t)(now - t_act) > idle_ticks) {  // idle here: counted
+                    uint64_t before = 0;
+                    if (t == 0) before = __hip_atomic_fetch_add(&ctl->idle, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    before = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)before) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(before >> 32)) << 32;
+                    idle = true;
+                    if (before + 1 >= gridDim.x) {  // every workgroup idle: the grid leaves
                         if (t == 0) __hip_atomic_fetch_max(&ctl->closing, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        why = 3;
                         break;
                     }
                 }
@@ -374,10 +403,17 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         if (t < 64) last = cmd & kJobMask;
     }
     if (t == 0) {
+        __hip_atomic_fetch_add(&ctl->why[why < kResExitReasons ? why : 0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (why == 4 && !idle) {  // gone on its quit bit: idle for the rest of the incarnation
+            const uint64_t b = __hip_atomic_fetch_add(&ctl->idle, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (b + 1 >= gridDim.x) __hip_atomic_fetch_max(&ctl->closing, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __hip_atomic_store(&sl->gone[part], inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t before = __hip_atomic_fetch_add(&ctl->exits, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (before + 1 == exit_base + gridDim.x)  // the grid's last workgroup
+        if (before + 1 == exit_base + gridDim.x) {  // the grid's last workgroup: the next starts with none idle
+            (void)__hip_atomic_exchange(&ctl->idle, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&mb->exited, inc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -572,6 +608,22 @@ public:
     uint64_t timeouts() const { return ld_acq(&timeouts_); }
     uint64_t withdrawn() const { return ld_acq(&withdrawn_); }
     int claimed() const { return __builtin_popcount(ld_acq(&claimed_)); }
+    // Workgroup exits so far by reason (ResCtl::why), read from device memory.
+    kmws_status exit_reasons(uint64_t* out, int n)
+    {
+        if (!dctl_) {
+            for (int i = 0; i < n; ++i) out[i] = 0;
+            return KMWS_OK;
+        }
+        uint64_t w[kResExitReasons] = {};
+        DevGuard g(device_);
+        if (hipMemcpy(w, dctl_->why, sizeof w, hipMemcpyDeviceToHost) != hipSuccess) {
+            (void)hipGetLastError();
+            return KMWS_ERR_FAILED;
+        }
+        for (int i = 0; i < n; ++i) out[i] = i < kResExitReasons ? w[i] : 0;
+        return KMWS_OK;
+    }
     int running() const
     {
         const uint64_t cur = ld_acq(&inc_);
@@ -674,8 +726,17 @@ private:
         std::memset(static_cast<void*>(mb_), 0, sizeof(ResMailbox));
         dmb_ = static_cast<ResMailbox*>(device_view(mb_));
         if (!dmb_) return KMWS_ERR_FAILED;
-        if (hipMalloc(reinterpret_cast<void**>(&dctl_), sizeof(ResCtl)) != hipSuccess ||
-            hipMemset(dctl_, 0, sizeof(ResCtl)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        // uncached: every XCD's workgroups read and update these words
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&dctl_), sizeof(ResCtl), hipDeviceMallocUncached) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            dctl_ = nullptr;
+            if (hipMalloc(reinterpret_cast<void**>(&dctl_), sizeof(ResCtl)) != hipSuccess) {
+                (void)hipGetLastError();
+                return KMWS_ERR_FAILED;
+            }
+        }
+        if (hipMemset(dctl_, 0, sizeof(ResCtl)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
             return KMWS_ERR_FAILED;
         }
@@ -934,6 +995,13 @@ kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_clai
     if (timeouts) *timeouts = w->timeouts();
     if (withdrawn) *withdrawn = w->withdrawn();
     return KMWS_OK;
+}
+
+kmws_status kmws_resident_exit_reasons(int device, uint64_t* counts, int n)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w || !counts || n < 0) return KMWS_ERR_INVALID_PARAM;
+    return w->exit_reasons(counts, n);
 }
 
 }  // extern "C"

@@ -49,6 +49,7 @@ EXPORTS = [
 BENCH_EXPORTS = [
     "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
     "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info", "kmws_resident_counters",
+    "kmws_resident_exit_reasons",
 ]
 
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)

@@ -202,12 +202,14 @@ bool mask_threads(int T, int active, size_t len, int calls)
             }
         });
     while (ready.load() < T) std::this_thread::yield();
-    uint64_t jobs0 = 0, jobs1 = 0, inc0 = 0, inc1 = 0;
+    uint64_t jobs0 = 0, jobs1 = 0, inc0 = 0, inc1 = 0, why0[5] = {}, why1[5] = {};
     kmws_resident_info(0, &jobs0, &inc0, nullptr);
+    kmws_resident_exit_reasons(0, why0, 5);
     const auto t0 = Clock::now();
     go.store(true, std::memory_order_release);
     while (done.load() < active) std::this_thread::yield();
     kmws_resident_info(0, &jobs1, &inc1, nullptr);
+    kmws_resident_exit_reasons(0, why1, 5);
     const double wall = secs(Clock::now() - t0);
     for (auto& x : th) x.join();
     std::vector<double> all;
@@ -225,10 +227,12 @@ bool mask_threads(int T, int active, size_t len, int calls)
     std::printf("{\"case\": \"mask_sync_threads\", \"codec\": \"kmws_resident\", \"threads\": %d, \"masking\": %d, "
                 "\"len\": %zu, \"calls_per_thread\": %d, \"us_median\": %.3f, \"us_p99\": %.3f, "
                 "\"calls_per_s\": %.0f, \"resident_jobs\": %llu, \"incarnations\": %llu, \"slot_median_us\": %s, "
-                "\"verified\": %s}\n",
+                "\"exits_lease_closing_resize_idle_quit\": [%llu, %llu, %llu, %llu, %llu], \"verified\": %s}\n",
                 T, active, len, calls, all[all.size() / 2] * 1e6, all[all.size() * 99 / 100] * 1e6,
                 (double)active * calls / wall, (unsigned long long)(jobs1 - jobs0), (unsigned long long)(inc1 - inc0),
-                per.c_str(), bad.load() == 0 ? "true" : "false");
+                per.c_str(), (unsigned long long)(why1[0] - why0[0]), (unsigned long long)(why1[1] - why0[1]),
+                (unsigned long long)(why1[2] - why0[2]), (unsigned long long)(why1[3] - why0[3]),
+                (unsigned long long)(why1[4] - why0[4]), bad.load() == 0 ? "true" : "false");
     std::fflush(stdout);
     return bad.load() == 0;
 }
