@@ -135,6 +135,7 @@ def bind(L: C.CDLL) -> C.CDLL:
         "kmws_check_unmasked": (i32, [u8p, u64, u64, vp, u32, vp, vp]),
         "kmws_resident_enable": (i32, [i32, i32]),
         "kmws_resident_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+        "kmws_resident_exit_reasons": (i32, [i32, C.POINTER(C.c_uint64), i32]),
         "kmws_resident_counters": (i32, [i32, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64),
                                          C.POINTER(C.c_uint64)]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
@@ -346,6 +347,19 @@ def resident_info(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
     return {"jobs": jobs.value, "launches": launches.value, "running": bool(running.value),
             "thread_slot": slot.value, "slots_claimed": claimed.value, "timeouts": tmo.value,
             "withdrawn": wd.value}
+
+
+RESIDENT_EXIT_REASONS = ("lease", "closing", "resize", "idle", "quit")
+
+
+def resident_exit_reasons(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
+    """kmws_resident_exit_reasons: the worker's workgroup exits so far by reason
+    (lease, closing = another workgroup found the grid idle, resize, idle =
+    this one completed the idle count, quit)."""
+    L = L or lib()
+    out = (C.c_uint64 * len(RESIDENT_EXIT_REASONS))()
+    _check(L.kmws_resident_exit_reasons(device, out, len(RESIDENT_EXIT_REASONS)), "kmws_resident_exit_reasons")
+    return dict(zip(RESIDENT_EXIT_REASONS, list(out)))
 
 
 def resident_enable(on: bool, device: int = 0) -> None:

@@ -520,6 +520,106 @@ def test_resident_worker_slot_per_thread():
     assert kmws.resident_info()["slots_claimed"] <= before["slots_claimed"], (before, kmws.resident_info())
 
 
+def test_resident_busy_grid_leaves_only_at_its_lease():
+    """Four threads masking 4 KiB back to back for ~30 ms: every workgroup exit
+    is a lease exit -- none decides the grid idle and none leaves on another's
+    idle decision (the first idle test compared workgroups' clocks and closed
+    busy grids every ~0.3 ms)."""
+    import threading
+    import time
+    rng = random.Random(31)
+    data = bytes(rng.randrange(256) for _ in range(4096))
+    start = threading.Barrier(5)
+    bad = []
+
+    def run(tid):
+        key = bytes([tid, 7, 9, 11])
+        want = orc.mask_bytes(key, data)
+        a = bytearray(data)
+        kmws.handle_data_mask(key, [a])  # claims the slot
+        start.wait()
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 0.03:
+            a = bytearray(data)
+            kmws.handle_data_mask(key, [a])
+            n += 1
+            if bytes(a) != want:
+                bad.append(tid)
+        start.wait()
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    start.wait()  # every thread holds its slot
+    before = kmws.resident_exit_reasons()
+    start.wait()  # every thread done
+    after = kmws.resident_exit_reasons()
+    for t in ths:
+        t.join()
+    d = {k: after[k] - before[k] for k in after}
+    print(f"\nexits while busy: {d}")
+    assert not bad
+    assert d["idle"] == 0 and d["closing"] == 0, d
+    assert d["lease"] >= 4 * 4 * 10, d  # ~30 incarnations of 4 slots x 4 parts
+
+
+def test_resident_slot_claimed_outside_the_grid_resizes_it():
+    """A thread keeps the grid busy; a second claims a slot the running
+    incarnation does not serve: the grid is asked to leave (a resize exit --
+    or, if that incarnation reached its lease first, the relaunch serves the
+    slot anyway), and every one of the late thread's 300 masks is exact.  (How
+    many of its calls launched shows in the C++ mask_threads rows, not here:
+    Python's timing includes the GIL the busy thread holds.)"""
+    import threading
+    import time
+    rng = random.Random(37)
+    data = bytes(rng.randrange(256) for _ in range(2048))
+    stop = threading.Event()
+    busy_started = threading.Event()
+
+    def busy():
+        key = b"\x01\x02\x03\x04"
+        want = orc.mask_bytes(key, data)
+        while not stop.is_set():
+            a = bytearray(data)
+            kmws.handle_data_mask(key, [a])
+            assert bytes(a) == want
+            busy_started.set()
+
+    tb = threading.Thread(target=busy)
+    tb.start()
+    busy_started.wait(5)
+    time.sleep(0.002)
+    res = {}
+
+    def late():
+        key = b"\x0a\x0b\x0c\x0d"
+        want = orc.mask_bytes(key, data)
+        before = kmws.resident_exit_reasons()
+        jobs0 = kmws.resident_info()["jobs"]
+        lat = []
+        for _ in range(300):
+            a = bytearray(data)
+            t0 = time.perf_counter()
+            kmws.handle_data_mask(key, [a])
+            lat.append(time.perf_counter() - t0)
+            assert bytes(a) == want
+        res["exits"] = {k: v - before[k] for k, v in kmws.resident_exit_reasons().items()}
+        res["slot"] = kmws.resident_info()["thread_slot"]
+        res["median_us"] = sorted(lat)[len(lat) // 2] * 1e6
+
+    tl = threading.Thread(target=late)
+    tl.start()
+    tl.join()
+    stop.set()
+    tb.join()
+    print(f"\nlate thread: {res}")
+    assert res["slot"] >= 0
+    assert res["exits"]["resize"] + res["exits"]["lease"] >= 1, res
+    assert res["median_us"] < 200, res
+
+
 def test_resident_more_threads_than_slots_launch_instead():
     """Twenty threads at once (the grid has 16 slots): the threads that find no
     free slot launch on their own streams instead of waiting; every result is
