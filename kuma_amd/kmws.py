@@ -395,6 +395,10 @@ class RxBatch:
     def pending(self) -> int:
         return lib().kmws_rx_batch_pending(self._b)
 
+    def pending_bytes(self) -> int:
+        """Masked payload bytes of the pending frames (kmws_rx_batch_pending_bytes)."""
+        return lib().kmws_rx_batch_pending_bytes(self._b)
+
     def submit(self) -> int:
         """kmws_rx_batch_submit: enqueue this generation's unmask, return at once."""
         r = lib().kmws_rx_batch_submit(self._b)

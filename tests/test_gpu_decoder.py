@@ -502,7 +502,11 @@ def test_resident_worker_slot_per_thread():
             lat.append(time.perf_counter() - t0)
             bad += bytes(a) != want
         res[tid] = (sorted(lat)[len(lat) // 2], bad, kmws.resident_info()["thread_slot"])
+        finish.wait()  # holds the slot until every thread has reported (a thread that
+        # exited early would free its slot for a late starter: the GIL can run one
+        # thread's 400 calls before another's first)
 
+    finish = threading.Barrier(4)
     before = kmws.resident_info()
     ths = [threading.Thread(target=run, args=(i,)) for i in (1, 2, 3, 4)]
     for t in ths:
@@ -520,16 +524,47 @@ def test_resident_worker_slot_per_thread():
     assert kmws.resident_info()["slots_claimed"] <= before["slots_claimed"], (before, kmws.resident_info())
 
 
+def test_rx_batch_pending_bytes_counts_masked_payloads():
+    """kmws_rx_batch_pending_bytes (what RxLoop keeps within the resident job
+    limits): the masked payload bytes fed since the last submit -- unmasked
+    frames and control payloads of length 0 not counted -- and 0 after a
+    submit; the frames then deliver exact."""
+    rng = random.Random(43)
+    b = kmws.RxBatch()
+    h = kmws.WSHandler(kmws.SERVER)
+    got = []
+    h.setFrameCallback(lambda hdr, data: got.append((hdr.opcode, data)))
+    wire, want, masked_bytes = b"", [], 0
+    for i, n in enumerate((100, 0, 5000, 70000, 7)):
+        payload = bytes(rng.randrange(256) for _ in range(n))
+        key = bytes(rng.randrange(256) for _ in range(4))
+        mask = i != 4  # the last one unmasked (a client-bound frame)
+        wire += orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=int(mask), maskey=key if mask else b"\0" * 4,
+                                          length=n)) + (orc.mask_bytes(key, payload) if mask else payload)
+        want.append((2, payload))
+        masked_bytes += n if mask else 0
+    assert b.pending_bytes() == 0
+    assert h.handleDataDeferred(b, wire[:-(7 + 2)]) in (0, 1)  # all but the unmasked frame
+    assert b.pending_bytes() == masked_bytes, (b.pending_bytes(), masked_bytes)
+    assert b.pending() == 4
+    assert b.submit() == 4
+    assert b.pending_bytes() == 0 and b.pending() == 0
+    b.poll(wait=True)
+    assert got == want[:4]
+
+
 def test_resident_busy_grid_leaves_only_at_its_lease():
-    """Four threads masking 4 KiB back to back for ~30 ms: every workgroup exit
-    is a lease exit -- none decides the grid idle and none leaves on another's
-    idle decision (the first idle test compared workgroups' clocks and closed
-    busy grids every ~0.3 ms)."""
+    """Four threads masking 4 KiB back to back: over ~30 ms of that (read while
+    they still run), every workgroup exit is a lease exit -- none decides the
+    grid idle and none leaves on another's idle decision (the first idle test
+    compared workgroups' clocks and closed busy grids every ~0.3 ms, DESIGN.md
+    sec.4)."""
     import threading
     import time
     rng = random.Random(31)
     data = bytes(rng.randrange(256) for _ in range(4096))
-    start = threading.Barrier(5)
+    ready = threading.Barrier(5)
+    stop = threading.Event()
     bad = []
 
     def run(tid):
@@ -537,31 +572,29 @@ def test_resident_busy_grid_leaves_only_at_its_lease():
         want = orc.mask_bytes(key, data)
         a = bytearray(data)
         kmws.handle_data_mask(key, [a])  # claims the slot
-        start.wait()
-        t0 = time.perf_counter()
-        n = 0
-        while time.perf_counter() - t0 < 0.03:
+        ready.wait()
+        while not stop.is_set():
             a = bytearray(data)
             kmws.handle_data_mask(key, [a])
-            n += 1
             if bytes(a) != want:
                 bad.append(tid)
-        start.wait()
 
     ths = [threading.Thread(target=run, args=(i,)) for i in range(4)]
     for t in ths:
         t.start()
-    start.wait()  # every thread holds its slot
+    ready.wait()  # every thread holds its slot and masks from now on
+    time.sleep(0.005)
     before = kmws.resident_exit_reasons()
-    start.wait()  # every thread done
+    time.sleep(0.03)
     after = kmws.resident_exit_reasons()
+    stop.set()
     for t in ths:
         t.join()
     d = {k: after[k] - before[k] for k in after}
     print(f"\nexits while busy: {d}")
     assert not bad
     assert d["idle"] == 0 and d["closing"] == 0, d
-    assert d["lease"] >= 4 * 4 * 10, d  # ~30 incarnations of 4 slots x 4 parts
+    assert d["lease"] >= 4 * 4 * 10, d  # ~30 incarnations of >= 4 slots x 4 parts
 
 
 def test_resident_slot_claimed_outside_the_grid_resizes_it():
