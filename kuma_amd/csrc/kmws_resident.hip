@@ -338,7 +338,10 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
             while ((uint64_t)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(127);
             if (t == 0 && (ld_sys(pw0) & kQuitBit)) s_cmd = 0;
             __syncthreads();
-            if (s_cmd == 0) break;
+            if (s_cmd == 0) {
+                why = 4;  // gone on its quit bit
+                break;
+            }
         }
 #endif
         if (t == 0) {
@@ -400,7 +403,10 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (t < 64) last = cmd & kJobMask;
+        if (t < 64) {
+            last = cmd & kJobMask;
+            t_act = wall_clock64();  // the slot was busy until now (a long job is not idle time)
+        }
     }
     if (t == 0) {
         __hip_atomic_fetch_add(&ctl->why[why < kResExitReasons ? why : 0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
