@@ -31,7 +31,13 @@
 // Every delivered payload is compared with what the client sent.  Prints one
 // JSON line per mode.  Test infrastructure (links the oracle): tests/test_abi_build.py.
 //
-// usage: loopback_cfg1 cpu|gpu|sync|adapter [reps] [frames per send iteration] [rx flush bytes] [variant] [connections]
+//   replay_cpu / replay_adapter  the server alone: each client replays the
+//        connection's masked wire image, built once before the run (remote
+//        peers' bytes: no codec work on this box's client side), and the server
+//        decodes with kuma's codec or with the drop-in's RxLoop adapter -- what
+//        a kuma server with the drop-in would meet; only the receive side
+//        crosses PCIe.
+// usage: loopback_cfg1 cpu|gpu|sync|adapter|replay_cpu|replay_adapter [reps] [frames per send iteration] [rx flush bytes] [variant] [connections]
 // (variant noresident: both loop threads switch their resident worker off --
 // every GPU job a launch and a wait, the A/B of kmws_resident.hip; submitpoll:
 // the gpu mode's flushes replaced by submit + poll(wait); inflight2: the
@@ -139,6 +145,8 @@ struct alignas(64) Times {
 
 struct alignas(64) Expect {  // one connection's (a line of its own: the server thread updates it per frame)
     std::vector<uint8_t> plain;  // kFrames * kLen
+    std::vector<uint8_t> wire;   // replay modes: every frame, header + masked payload
+    std::vector<size_t> frame_off;  // where frame k starts in `wire` (kFrames + 1 entries)
     std::atomic<int> got{0};
     std::atomic<int> bad{0};
 };
@@ -200,6 +208,7 @@ struct LoopObjs {
 bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
 bool g_noresident = false;
 bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flushes
+bool g_replay = false;      // replay_* modes: clients replay a pre-built masked wire image
 int g_inflight = 1;         // adapter mode: the TxLoop's generations in flight after a run (inflight2: 2)
 size_t g_tx_ring = (size_t)1 << 20;  // adapter mode: the TxLoop's pinned send ring (ring16m: 16 MiB)
 
@@ -369,7 +378,18 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     kmws_tx_batch* tx = lo.tx;
     uint8_t* sring = lo.sring;
     std::vector<uint8_t> sbuf;
-    if (!gpu || g_sync) sbuf.resize(kGroup * kLen);
+    // the client's codec (replay modes: none, the wire image is pre-built)
+    const bool cgpu = gpu && !g_replay, cadapter = adapter && !g_replay;
+    if (g_replay) {
+        for (int g0 = 0; g0 < kFrames; g0 += kGroup) {  // one loop iteration: the next kGroup frames' bytes
+            const int ng = std::min(kGroup, kFrames - g0);
+            std::vector<iovec> one(1, iovec{e.wire.data() + e.frame_off[g0], e.frame_off[g0 + ng] - e.frame_off[g0]});
+            const double tt = now_s();
+            send_all(fd, one);
+            T.writev += now_s() - tt;
+        }
+    }
+    if (!cgpu || g_sync) sbuf.resize(kGroup * kLen);
     std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hdrs(kGroup);
     std::vector<int> hlen(kGroup);
     std::vector<iovec> iov;
@@ -377,7 +397,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     const double cc0 = thread_cpu_s();
     rusage ru0{};
     getrusage(RUSAGE_THREAD, &ru0);
-    if (adapter) {
+    if (cadapter) {
         // the client loop thread: its TxLoop (the posted task masks the
         // iteration's sends with one GPU job and writes finished generations)
         std::vector<kmws::TxLoop::Task> ctasks;
@@ -416,9 +436,9 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         if (txl.close(conn) < 0) std::exit(7);  // the last generations: masked and written
         T.tx_flush += now_s() - tt - (T.writev - w0);
     }
-    for (int g0 = 0; g0 < kFrames && !adapter; g0 += kGroup) {
+    for (int g0 = 0; g0 < kFrames && !cadapter && !g_replay; g0 += kGroup) {
         const int ng = std::min(kGroup, kFrames - g0);
-        uint8_t* base = gpu && !g_sync ? sring : sbuf.data();
+        uint8_t* base = cgpu && !g_sync ? sring : sbuf.data();
         // the application writes its payloads (the send buffer is reused per iteration)
         std::memcpy(base, e.plain.data() + (size_t)g0 * kLen, (size_t)ng * kLen);
         for (int j = 0; j < ng; ++j) {
@@ -434,7 +454,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
                 if (kmws::ws::WSHandler::handleDataMask(h.maskey, p, kLen) != KMWS_OK) std::exit(7);
                 h.length = (uint32_t)kLen;
                 hlen[j] = kmws::ws::WSHandler::encodeFrameHeader(h, hdrs[j].data());
-            } else if (gpu) {
+            } else if (cgpu) {
                 kmws_frame_hdr h;
                 std::memset(&h, 0, sizeof h);
                 h.fin = 1;
@@ -456,10 +476,10 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             }
         }
         double tt = now_s();
-        if (gpu && !g_sync && g_submitpoll) {
+        if (cgpu && !g_sync && g_submitpoll) {
             const int64_t tk = kmws_tx_batch_submit(tx);
             if (tk <= 0 || kmws_tx_batch_poll(tx, tk, 1) != 1) std::exit(7);
-        } else if (gpu && !g_sync && kmws_tx_batch_flush(tx) != ng) {
+        } else if (cgpu && !g_sync && kmws_tx_batch_flush(tx) != ng) {
             std::exit(7);
         }
         T.tx_flush += now_s() - tt;
@@ -483,7 +503,7 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     rusage ru1{};
     getrusage(RUSAGE_THREAD, &ru1);
     T.client_nivcsw = ru1.ru_nivcsw - ru0.ru_nivcsw;
-    if (gpu) kmws_resident_counters(0, &T.client_slot, nullptr, nullptr, nullptr);
+    if (cgpu) kmws_resident_counters(0, &T.client_slot, nullptr, nullptr, nullptr);
     server.join();
     close(fd);
     close(ls);
@@ -506,7 +526,8 @@ int main(int argc, char** argv)
     if (argc > 5 && std::string(argv[5]) == "ring16m") g_tx_ring = (size_t)16 << 20;
     const int conns = argc > 6 ? std::max(1, std::min(8, std::atoi(argv[6]))) : 1;
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
-    const bool adapter = mode == "adapter";
+    g_replay = mode == "replay_cpu" || mode == "replay_adapter";
+    const bool adapter = mode == "adapter" || mode == "replay_adapter";
     g_sync = mode == "sync";
     const bool gpu = mode == "gpu" || adapter || g_sync;
     if (gpu && kmws_device_count() < 1) {
@@ -522,8 +543,31 @@ int main(int argc, char** argv)
     std::vector<Expect> es(conns);
     std::vector<LoopObjs> los(conns);
     std::vector<Times> ts(conns);
+    std::vector<uint8_t> wire;  // the masked wire image the replay clients send
+    std::vector<size_t> frame_off;
+    if (g_replay) {
+        for (int f = 0; f < kFrames; ++f) {
+            frame_off.push_back(wire.size());
+            orc_hdr h;
+            std::memset(&h, 0, sizeof h);
+            h.fin = 1;
+            h.opcode = 1;
+            h.mask = 1;
+            std::memcpy(h.maskey, &keys[f], 4);
+            h.length = (uint32_t)kLen;
+            uint8_t hb[14];
+            const int hl = orc_encode_header(&h, hb);
+            wire.insert(wire.end(), hb, hb + hl);
+            const size_t p0 = wire.size();
+            wire.insert(wire.end(), plain.begin() + (size_t)f * kLen, plain.begin() + (size_t)(f + 1) * kLen);
+            orc_mask(h.maskey, wire.data() + p0, kLen, 0);
+        }
+        frame_off.push_back(wire.size());
+    }
     for (int c = 0; c < conns; ++c) {
         es[c].plain = plain;
+        es[c].wire = wire;
+        es[c].frame_off = frame_off;
         if (!gpu) continue;
         LoopObjs& lo = los[c];
         lo.rx = kmws_rx_batch_create(0);

@@ -105,11 +105,12 @@ def test_loopback_cfg1_cpu_codec(tmp_path):
 def test_loopback_cfg1_cpu_codec_three_connections(tmp_path):
     """Three client / server loop-thread pairs at once, 1,000 frames each."""
     import json
-    r = subprocess.run([str(_build_loopback(tmp_path)), "cpu", "2", "16", "0", "0", "3"], capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["verified"] and d["connections"] == 3
+    exe = _build_loopback(tmp_path)
+    for mode in ("cpu", "replay_cpu"):  # replay_cpu: clients replay a pre-built masked wire image
+        r = subprocess.run([str(exe), mode, "2", "16", "0", "0", "3"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["verified"] and d["connections"] == 3 and d["mode"] == mode
 
 
 @pytest.mark.gpu
@@ -153,11 +154,13 @@ def test_loopback_cfg1_adapter_batched(tmp_path):
 @pytest.mark.gpu
 def test_loopback_cfg1_four_connections_share_the_resident_worker(tmp_path):
     """Four connections at once, each with its own client and server loop thread
-    (eight threads holding resident slots): the adapter, the loop-batched mode and
-    the synchronous member swap deliver every payload of every connection intact."""
+    (eight threads holding resident slots): the adapter, the loop-batched mode,
+    the synchronous member swap and the adapter's server alone (replay_adapter:
+    clients replay a pre-built masked wire image) deliver every payload of every
+    connection intact."""
     import json
     exe = _build_loopback(tmp_path)
-    for mode in ("adapter", "gpu", "sync"):
+    for mode in ("adapter", "gpu", "sync", "replay_adapter"):
         r = subprocess.run([str(exe), mode, "2", "16", "0", "0", "4"], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])

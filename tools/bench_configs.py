@@ -82,7 +82,9 @@ def loopback(reps: int):
     """tests/cpp/loopback_cfg1.cpp over a real loopback socket (BASELINE
     configs[0]): kuma's codec (oracle) on both ends vs the synchronous member
     swap, the loop-batched gpu mode and the RxLoop adapter, 16 and 64 frames per
-    send iteration."""
+    send iteration; 1-8 connections at once; and the server alone (replay_*:
+    clients replay a pre-built masked wire image, the server runs kuma's codec
+    or the drop-in)."""
     import subprocess
     import tempfile
     from kuma_amd import build as kb
@@ -106,8 +108,11 @@ def loopback(reps: int):
                 for x in got:
                     x["variant"] = extra[1] if extra else ""
                 rows += got
+        for mode in ("replay_cpu", "replay_adapter"):  # the server alone (clients replay a masked image)
+            r = subprocess.run([exe, mode, str(reps), "16"], capture_output=True, text=True, timeout=300)
+            rows += [dict(json.loads(x), variant="") for x in r.stdout.strip().splitlines() if x.startswith("{")]
         for conns in ("2", "4", "8"):  # loop-thread pairs at once, 64 KiB per send iteration
-            for mode in ("cpu", "sync", "gpu", "adapter"):
+            for mode in ("cpu", "sync", "gpu", "adapter", "replay_cpu", "replay_adapter"):
                 r = subprocess.run([exe, mode, str(reps), "16", "0", "0", conns], capture_output=True, text=True,
                                    timeout=300)
                 got = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
