@@ -37,7 +37,11 @@
 //        decodes with kuma's codec or with the drop-in's RxLoop adapter -- what
 //        a kuma server with the drop-in would meet; only the receive side
 //        crosses PCIe.
-// usage: loopback_cfg1 cpu|gpu|sync|adapter|replay_cpu|replay_adapter [reps] [frames per send iteration] [rx flush bytes] [variant] [connections]
+//   sink_cpu / sink_adapter  the client alone: it sends with kuma's codec or with
+//        the drop-in's TxLoop, and the server only reads and compares the bytes
+//        with the expected masked wire image (no decode) -- a kuma client's
+//        send side; only it crosses PCIe.
+// usage: loopback_cfg1 cpu|gpu|sync|adapter|replay_cpu|replay_adapter|sink_cpu|sink_adapter [reps] [frames per send iteration] [rx flush bytes] [variant] [connections]
 // (variant noresident: both loop threads switch their resident worker off --
 // every GPU job a launch and a wait, the A/B of kmws_resident.hip; submitpoll:
 // the gpu mode's flushes replaced by submit + poll(wait); inflight2: the
@@ -209,6 +213,7 @@ bool g_sync = false;  // mode "sync": the synchronous member swap on both ends
 bool g_noresident = false;
 bool g_submitpoll = false;  // gpu mode: submit + poll(wait) instead of the flushes
 bool g_replay = false;      // replay_* modes: clients replay a pre-built masked wire image
+bool g_sink = false;        // sink_* modes: the server compares the bytes with that image, no decode
 int g_inflight = 1;         // adapter mode: the TxLoop's generations in flight after a run (inflight2: 2)
 size_t g_tx_ring = (size_t)1 << 20;  // adapter mode: the TxLoop's pinned send ring (ring16m: 16 MiB)
 
@@ -238,7 +243,21 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
         ready = true;
         const double sc0 = thread_cpu_s();
-        if (g_sync) {
+        if (g_sink) {  // reads compared with the expected wire image; a frame counted per frame's bytes
+            std::vector<uint8_t> buf(kRead);
+            size_t pos = 0;
+            const size_t total = e.wire.size();
+            while (pos < total) {
+                double t = now_s();
+                const ssize_t r = recv(fd, buf.data(), kRead, 0);
+                T.recv += now_s() - t;
+                if (r <= 0) break;
+                if ((size_t)r > total - pos || std::memcmp(buf.data(), e.wire.data() + pos, (size_t)r) != 0)
+                    e.bad.fetch_add(1);
+                pos += (size_t)r;
+            }
+            e.got.store(pos == total ? kFrames : 0, std::memory_order_release);
+        } else if (g_sync) {
             kmws::ws::WSHandler h;  // per connection; no RxLoop: one synchronous GPU job per read
             h.setMode(kmws::ws::WSMode::SERVER);
             h.setInPlace(false);
@@ -380,6 +399,14 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
     std::vector<uint8_t> sbuf;
     // the client's codec (replay modes: none, the wire image is pre-built)
     const bool cgpu = gpu && !g_replay, cadapter = adapter && !g_replay;
+    if (!cgpu || g_sync) sbuf.resize(kGroup * kLen);
+    std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hdrs(kGroup);
+    std::vector<int> hlen(kGroup);
+    std::vector<iovec> iov;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double cc0 = thread_cpu_s();
+    rusage ru0{};
+    getrusage(RUSAGE_THREAD, &ru0);
     if (g_replay) {
         for (int g0 = 0; g0 < kFrames; g0 += kGroup) {  // one loop iteration: the next kGroup frames' bytes
             const int ng = std::min(kGroup, kFrames - g0);
@@ -389,14 +416,6 @@ double run_once(bool gpu, bool adapter, Expect& e, const std::vector<uint32_t>& 
             T.writev += now_s() - tt;
         }
     }
-    if (!cgpu || g_sync) sbuf.resize(kGroup * kLen);
-    std::vector<std::array<uint8_t, KMWS_MAX_HEADER_SIZE>> hdrs(kGroup);
-    std::vector<int> hlen(kGroup);
-    std::vector<iovec> iov;
-    const auto t0 = std::chrono::steady_clock::now();
-    const double cc0 = thread_cpu_s();
-    rusage ru0{};
-    getrusage(RUSAGE_THREAD, &ru0);
     if (cadapter) {
         // the client loop thread: its TxLoop (the posted task masks the
         // iteration's sends with one GPU job and writes finished generations)
@@ -527,7 +546,8 @@ int main(int argc, char** argv)
     const int conns = argc > 6 ? std::max(1, std::min(8, std::atoi(argv[6]))) : 1;
     if (g_noresident) kmws_resident_enable(0, 0);  // the client (main) thread
     g_replay = mode == "replay_cpu" || mode == "replay_adapter";
-    const bool adapter = mode == "adapter" || mode == "replay_adapter";
+    g_sink = mode == "sink_cpu" || mode == "sink_adapter";
+    const bool adapter = mode == "adapter" || mode == "replay_adapter" || mode == "sink_adapter";
     g_sync = mode == "sync";
     const bool gpu = mode == "gpu" || adapter || g_sync;
     if (gpu && kmws_device_count() < 1) {
@@ -545,7 +565,7 @@ int main(int argc, char** argv)
     std::vector<Times> ts(conns);
     std::vector<uint8_t> wire;  // the masked wire image the replay clients send
     std::vector<size_t> frame_off;
-    if (g_replay) {
+    if (g_replay || g_sink) {
         for (int f = 0; f < kFrames; ++f) {
             frame_off.push_back(wire.size());
             orc_hdr h;

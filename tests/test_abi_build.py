@@ -106,7 +106,7 @@ def test_loopback_cfg1_cpu_codec_three_connections(tmp_path):
     """Three client / server loop-thread pairs at once, 1,000 frames each."""
     import json
     exe = _build_loopback(tmp_path)
-    for mode in ("cpu", "replay_cpu"):  # replay_cpu: clients replay a pre-built masked wire image
+    for mode in ("cpu", "replay_cpu", "sink_cpu"):  # replay: clients replay a masked image; sink: no decode
         r = subprocess.run([str(exe), mode, "2", "16", "0", "0", "3"], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -160,7 +160,7 @@ def test_loopback_cfg1_four_connections_share_the_resident_worker(tmp_path):
     connection intact."""
     import json
     exe = _build_loopback(tmp_path)
-    for mode in ("adapter", "gpu", "sync", "replay_adapter"):
+    for mode in ("adapter", "gpu", "sync", "replay_adapter", "sink_adapter"):
         r = subprocess.run([str(exe), mode, "2", "16", "0", "0", "4"], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])

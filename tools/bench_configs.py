@@ -108,11 +108,11 @@ def loopback(reps: int):
                 for x in got:
                     x["variant"] = extra[1] if extra else ""
                 rows += got
-        for mode in ("replay_cpu", "replay_adapter"):  # the server alone (clients replay a masked image)
+        for mode in ("replay_cpu", "replay_adapter", "sink_cpu", "sink_adapter"):  # the server alone / the client alone
             r = subprocess.run([exe, mode, str(reps), "16"], capture_output=True, text=True, timeout=300)
             rows += [dict(json.loads(x), variant="") for x in r.stdout.strip().splitlines() if x.startswith("{")]
         for conns in ("2", "4", "8"):  # loop-thread pairs at once, 64 KiB per send iteration
-            for mode in ("cpu", "sync", "gpu", "adapter", "replay_cpu", "replay_adapter"):
+            for mode in ("cpu", "sync", "gpu", "adapter", "replay_cpu", "replay_adapter", "sink_cpu", "sink_adapter"):
                 r = subprocess.run([exe, mode, str(reps), "16", "0", "0", conns], capture_output=True, text=True,
                                    timeout=300)
                 got = [json.loads(x) for x in r.stdout.strip().splitlines() if x.startswith("{")]
