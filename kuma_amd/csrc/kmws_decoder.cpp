@@ -818,6 +818,12 @@ int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
 {
     if (!b) return KMWS_ERR_INVALID_PARAM;
     const int64_t nf = (int64_t)b->frames.size();
+    // what is in flight first: the thread's resident slot holds one job, and a
+    // job posted while the previous one runs launches instead
+    if (!b->inflight.empty()) {
+        const int r0 = kmws_tx_batch_poll(b, b->next_ticket - 1, 1);
+        if (r0 < 0) return r0;
+    }
     const int64_t t = tx_submit(b, true);  // masked when it returns: the poll only copies back
     if (t < 0) return t;
     const int r = kmws_tx_batch_poll(b, b->next_ticket - 1, 1);
@@ -990,9 +996,17 @@ int kmws_rx_batch_poll(kmws_rx_batch* b, int wait)
 
 int kmws_rx_batch_flush(kmws_rx_batch* b)
 {
+    // the generations in flight first (delivered in order, before this one):
+    // the thread's resident slot holds one job, and a job posted while the
+    // previous one runs launches instead (the loopback's ring-wrap flushes did)
+    int d0 = 0;
+    if (b && !b->flushing && !b->inflight.empty()) {
+        d0 = kmws_rx_batch_poll(b, 1);
+        if (d0 < 0) return d0;
+    }
     const int s = rx_submit(b, true);
     const int d = kmws_rx_batch_poll(b, 1);
-    return s < 0 ? s : d;
+    return s < 0 ? s : d < 0 ? d : d0 + d;
 }
 
 }  // extern "C"
