@@ -39,9 +39,17 @@ def parse():
                    help="GPUs (ranks) of this node. Without WORLD_SIZE in the environment bench.py starts the N "
                         "rank processes itself (one per GPU, before any GPU call); under torchrun WORLD_SIZE "
                         "must equal N")
-    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg1"],
+    p.add_argument("--config", default="cfg2", choices=["cfg2", "cfg1", "e2e"],
                    help="cfg2 (default): the headline device-resident unmask; cfg1: kuma's CPU case "
-                        "(1,000 x 4 KiB frames in 64 KiB reads) with its cpu_baseline")
+                        "(1,000 x 4 KiB frames in 64 KiB reads) with its cpu_baseline; e2e: host-resident "
+                        "frames end to end (pinned H2D -> kernel -> D2H), each rank its own shard through its "
+                        "own pinned staging and kmws_pipeline (SURVEY 8 e), --e2e-gib per rank")
+    p.add_argument("--cfg5-anchor", type=int, default=1,
+                   help="N = 1 cfg2 run: also time BASELINE configs[4]'s whole job (cfg5_job key), the same-job "
+                        "anchor of the N > 1 curve (0 = skip)")
+    p.add_argument("--e2e-gib", type=float, default=2.0,
+                   help="host-resident end-to-end shard per rank in GiB: the e2e_host key of a cfg2 run "
+                        "(0 = skip), or the workload of --config e2e")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
@@ -551,51 +559,152 @@ def plain_rate(kmws, torch, dev, n, L, descs, ws, schedule, seed, steps, warmup,
     return out
 
 
-def main():
-    a = parse()
-    if a.config == "cfg1":
-        print(json.dumps(run_cfg1(max(a.steps, 10))), flush=True)
-        return
-    env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and a.gpus > 1:
-        sys.exit(launch_ranks(a.gpus))
-    world = int(env_world or "1")
-    if world != a.gpus:
-        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU, the two must agree")
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    job_frames = a.job_frames if a.job_frames is not None else (CFG5_JOB_FRAMES if world > 1 else 0)
+E2E_METRIC = ("GiB/s host-resident WS frame unmask end to end (pinned H2D -> unmask kernel -> D2H), "
+              "64 KiB frames")
+E2E_HDR = 14  # a masked 64 KiB frame's header (WSHandler.cpp:46-106: 2 + 8 + 4)
 
-    import torch
-    import torch.distributed as dist
-    from kuma_amd import kmws
 
-    ndev = torch.cuda.device_count()
-    if ndev < 1:
-        raise SystemExit("bench: no GPU visible; the HIP path has no CPU fallback")
-    dev = torch.device("cuda", local % ndev)  # one GPU per rank; modulo only when rehearsing on fewer GPUs
-    shared_gpu = world > ndev  # a rehearsal: several ranks on one GPU (gloo)
-    torch.cuda.set_device(dev)
+def _splitmix32(seed: int, n: int):
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = np.arange(n, dtype=np.uint64) + np.uint64(seed & (2**64 - 1)) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev, gib=None, steps=None, warmup=None):
+    """The host-resident path on N GPUs (SURVEY 8 e, f-3).
+    kuma's frames start and end in host memory (a socket read on a loop
+    thread, TcpConnection.cpp:229).  Each rank holds its own shard -- `gib` GiB
+    of masked 64 KiB frames in a pinned host wire image (14-byte headers between
+    payloads, as they arrive) allocated with kmws_host_alloc on its own GPU --
+    and unmasks it in place end to end through its own kmws_pipeline (a 3-slot
+    SDMA ring: H2D || unmask kernel || D2H on three streams, 64 MiB chunks), so
+    every rank's payload crosses its own GPU's PCIe link twice into its own
+    staging.  No data-path collective; host DRAM is what the ranks share.
+    value = all ranks' payload over the slowest rank's time (weak scaling: a
+    fixed shard per rank).  Each rank also times raw pinned H2D and D2H copies
+    of 1 GiB with every rank copying at once (its share of PCIe and host DRAM
+    under the same concurrency).  Every byte of every shard is verified on the
+    device after an odd number of passes (payload unmasked, headers untouched).
+    Returns rank 0's record (None on other ranks)."""
+    import ctypes as C
+    import numpy as np
+    gib = a.e2e_gib if gib is None else gib
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
+    L, H = 65536, E2E_HDR
+    stride = L + H
+    n = max(1, int(gib * 2**30) // stride)
+    span = n * stride
+    seed = (a.seed ^ 0xE2E0) + rank * (span >> 3)  # the shards are slices of one job
+    K = kmws.lib()
+    ptr = K.kmws_host_alloc(span, dev.index)
+    if not ptr:
+        raise RuntimeError(f"kmws_host_alloc({span}) failed on rank {rank}")
+    try:
+        host = torch.from_numpy(np.ctypeslib.as_array((C.c_uint8 * span).from_address(ptr)))
+        scratch = torch.empty(span, dtype=torch.uint8, device=dev)
+
+        def barrier():
+            if world > 1:
+                dist.barrier()
+
+        # raw pinned copies, every rank at once (before the shard is written)
+        cb = min(1 << 30, span)
+        rates = {}
+        for name, (dst, src) in (("h2d", (scratch[:cb], host[:cb])), ("d2h", (host[:cb], scratch[:cb]))):
+            best = 1e9
+            for _ in range(3):
+                barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                dst.copy_(src, non_blocking=True)
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t0)
+            rates[name] = cb / best / 2**30
+        # the shard: synthetic bytes everywhere, frame i's payload at i * stride + H
+        kmws.fill_synthetic(scratch, seed)
+        host.copy_(scratch)
+        torch.cuda.synchronize()
+        d = np.zeros(n, dtype=[("off", "<u8"), ("len", "<u4"), ("key", "<u4")])
+        d["off"] = np.arange(n, dtype=np.uint64) * stride + H
+        d["len"] = L
+        d["key"] = _splitmix32((a.seed ^ 0x5EED) + rank * n, n)
+        chunk = 64 << 20
+        pipe = kmws.Pipeline(dev.index, chunk, 1 << 16, 3, transfer=kmws.Pipeline.COPY)
+        for _ in range(warmup):
+            pipe.unmask(host, d)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pipe.unmask(host, d)
+        elapsed = time.perf_counter() - t0
+        barrier()
+        passes = warmup + steps
+        if passes % 2 == 0:  # an odd count leaves the payloads unmasked: what the checker expects
+            pipe.unmask(host, d)
+        scratch.copy_(host)
+        descs = kmws.make_descs(d["off"].astype(np.int64), d["len"].astype(np.int64), d["key"].astype(np.int64),
+                                device=dev)
+        mism = kmws.check_unmasked(scratch, seed, descs)
+        del pipe
+    finally:
+        torch.cuda.synchronize()
+        scratch = host = None
+        K.kmws_host_free(ptr)
+        torch.cuda.empty_cache()
+    me = {"rank": rank, "device": dev.index, "frames": n, "host_bytes": span, "elapsed_s": round(elapsed, 4),
+          "payload_GiB_s": round(n * L * steps / elapsed / 2**30, 2), "raw_h2d_GiB_s": round(rates["h2d"], 2),
+          "raw_d2h_GiB_s": round(rates["d2h"], 2), "byte_mismatches": mism}
+    ranks = [me]
     if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-    coll_dev = dev if a.dist_backend == "nccl" else torch.device("cpu")
-    if kmws.device_count() < 1:
-        raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    if rank != 0:
+        return None
+    total_mism = sum(r["byte_mismatches"] for r in ranks)
+    payload = n * L * world
+    value = payload * steps / elapsed / 2**30
+    raw = min(min(r["raw_h2d_GiB_s"], r["raw_d2h_GiB_s"]) for r in ranks)
+    return {"metric": E2E_METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(elapsed * 1e3 / steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (device-generated splitmix64 bytes copied into pinned host memory, per-frame keys)",
+            "config": {"workload": "host-resident end to end: per rank %d x 64 KiB masked frames in a pinned host "
+                                   "wire image (14-B headers between payloads), in-place unmask through the rank's "
+                                   "own kmws_pipeline (3-slot SDMA ring, H2D || kernel || D2H)" % n,
+                       "frames_per_gpu": n, "host_bytes_per_gpu": span, "chunk_MiB": chunk >> 20,
+                       "transfer": "copy (SDMA ring)", "ranks_share_one_gpu": world > ndev,
+                       "parallelism": f"shard per rank x{world}, own PCIe link and pinned staging, no collective",
+                       "dist_backend": a.dist_backend if world > 1 else None},
+            "pcie": {"bytes_per_step_per_gpu": 2 * span, "note": "each shard crosses PCIe twice (H2D of the "
+                     "chunk, D2H of its frames' extent: at most 2 x the wire image)",
+                     "payload_frac_of_concurrent_raw_copy": round(value / world / raw, 3) if raw else None},
+            "ranks": ranks, "verify": {"byte_mismatches": total_mism, "ok": total_mism == 0},
+            "shared_limit": "host DRAM: every rank's H2D reads and D2H writes land in the same sockets' memory; "
+                            "compare raw_h2d / raw_d2h per rank at N with N = 1"}
 
+
+def run_job(a, kmws, torch, dist, dev, coll_dev, rank, world, job_frames, shared_gpu, with_plain=True):
+    """One pass of the device-resident unmask over a job: `job_frames` frames
+    split over the ranks (strong scaling, BASELINE configs[4]), or 0 = a.frames
+    per rank (weak, configs[1]).  A rank's shard larger than one resident batch
+    runs as sub-batches (the same count on every rank), each generated on the
+    device untimed, then timed between barriers; the step time is the sum over
+    sub-batches.  Returns the rank-0 facts (every rank returns them)."""
     from kuma_amd import shard
     L = a.frame_len
-    # The job: world x frames (weak scaling, N = 1 default: cfg2) or a fixed job
-    # of J frames split over the ranks (strong scaling, BASELINE configs[4]: 10 M
-    # frames on 1..8 GPUs, the N > 1 default).  Rank g owns global frames [lo, hi)
-    # (kuma_amd/shard.py); payload and keys are generated from global positions,
-    # so the shards are slices of one big job.
+    # Rank g owns global frames [lo, hi) (kuma_amd/shard.py); payload and keys are
+    # generated from global positions, so the shards are slices of one big job.
     job = job_frames if job_frames else a.frames * world
     g_lo, g_hi = shard.uniform_range(job, rank, world)
-    # A shard larger than one resident batch runs as sub-batches (same count on
-    # every rank), each generated on device untimed, then timed like one batch.
     n, batches = shard.sub_batches(job, rank, world, a.max_batch_frames)
     nb = len(batches)
     span = n * L
@@ -605,7 +714,7 @@ def main():
     if a.placement == "probe" and not shared_gpu:
         arena, base_all, placement = place_batch(kmws, torch, dev, span, a.placement_slack_gib << 30)
     elif shared_gpu:
-        placement["why"] = f"{world} ranks share {ndev} GPU(s): rehearsal, no arena"
+        placement["why"] = f"{world} ranks share one GPU: rehearsal, no arena"
     arena_used = arena  # None: the timed batch is a plain allocation
     if arena is None:
         base_all = torch.empty(span, dtype=torch.uint8, device=dev)
@@ -665,10 +774,9 @@ def main():
     alg_bytes = alg_total // max(launches, 1)
 
     plain = None
-    if world == 1 and not a.no_plain and arena is not None:
+    if with_plain and world == 1 and not a.no_plain and arena is not None:
         # the same schedule on a plain allocation: the headline is not a best-of-placements number alone
-        del base_all, base
-        arena = None
+        base_all = base = arena = None
         torch.cuda.empty_cache()
         b_lo, b_hi = batches[0]
         plain = plain_rate(kmws, torch, dev, b_hi - b_lo, L, descs[:b_hi - b_lo], ws, schedule,
@@ -689,21 +797,103 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, per_rank[0])
         per_rank = gathered
-    if a.no_verify:
-        mismatches = None
+    base_all = base = descs = ws = arena = None  # the next job (cfg5_job, e2e_host) gets the HBM back
+    torch.cuda.empty_cache()
+    return {"job": job, "n": n, "nb": nb, "g_lo": g_lo, "g_hi": g_hi, "elapsed": elapsed, "kern_ms": kern_ms,
+            "alg_bytes": alg_bytes, "mismatches": None if a.no_verify else mismatches, "status": st,
+            "schedule": schedule, "placement": placement, "arena_used": arena_used is not None, "plain": plain,
+            "ranks": per_rank,
+            # payload GiB/s of the whole job (all ranks) over the slowest rank's time
+            "value": job * L * a.steps / elapsed / 2**30, "ms_per_step": elapsed * 1e3 / a.steps}
 
-    ms_per_step = elapsed * 1e3 / a.steps  # one step = one pass over the rank's shard
-    total_payload = job * L
-    value = total_payload * a.steps / elapsed / 2**30  # = shard.aggregate_rate over ranks (elapsed = max)
+
+def main():
+    a = parse()
+    if a.config == "cfg1":
+        print(json.dumps(run_cfg1(max(a.steps, 10))), flush=True)
+        return
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    world = int(env_world or "1")
+    if world != a.gpus:
+        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU, the two must agree")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    job_frames = a.job_frames if a.job_frames is not None else (CFG5_JOB_FRAMES if world > 1 else 0)
+
+    import torch
+    import torch.distributed as dist
+    from kuma_amd import kmws
+
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench: no GPU visible; the HIP path has no CPU fallback")
+    dev = torch.device("cuda", local % ndev)  # one GPU per rank; modulo only when rehearsing on fewer GPUs
+    shared_gpu = world > ndev  # a rehearsal: several ranks on one GPU (gloo)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = dev if a.dist_backend == "nccl" else torch.device("cpu")
+    if kmws.device_count() < 1:
+        raise SystemExit("bench: no gfx950 device visible; the HIP path has no CPU fallback")
+
+    if a.config == "e2e":
+        out = run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        if out is not None and not out["verify"]["ok"]:
+            raise SystemExit("bench: e2e verification failed")
+        return
+
+    L = a.frame_len
+    r = run_job(a, kmws, torch, dist, dev, coll_dev, rank, world, job_frames, shared_gpu)
+    # At N = 1 the headline is cfg2 (weak); the N > 1 lines run BASELINE
+    # configs[4]'s fixed job (strong).  So that the 1 -> 8 curve has a same-job
+    # anchor, N = 1 also times that job, its 8 resident
+    # sub-batches timed exactly as N > 1 times its ranks' sub-batches.
+    cfg5 = None
+    if world == 1 and not job_frames and a.cfg5_anchor:
+        c = run_job(a, kmws, torch, dist, dev, coll_dev, rank, world, CFG5_JOB_FRAMES, shared_gpu, with_plain=False)
+        cfg5 = {"value": round(c["value"], 2), "unit": "GiB/s", "ms_per_step": round(c["ms_per_step"], 4),
+                "total_frames": c["job"], "frame_len": L, "resident_batch_frames": c["n"], "sub_batches": c["nb"],
+                "kernel_ms": round(c["kern_ms"], 4), "unmask_schedule": c["schedule"],
+                "frac": round(c["alg_bytes"] / (c["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "verify": {"status_word": c["status"], "byte_mismatches": c["mismatches"]}, "ranks": c["ranks"],
+                "scaling": "strong",
+                "note": "BASELINE configs[4]'s whole job on this one GPU, timed as bench.py --gpus N times it: "
+                        "per sub-batch, generated on device untimed, barrier + synchronize around the timed "
+                        "steps, step time = sum over sub-batches; the N > 1 lines' value over this value is "
+                        "their speed-up"}
+    e2e = None
+    if a.e2e_gib > 0:
+        try:
+            e2e = run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev, gib=a.e2e_gib,
+                          steps=min(a.steps, 5), warmup=1)
+        except Exception as ex:  # recorded, never masking the headline
+            e2e = {"error": repr(ex)}
+
+    ms_per_step = r["ms_per_step"]
+    value = r["value"]  # = shard.aggregate_rate over ranks (elapsed = max)
+    kern_ms, alg_bytes, schedule, plain = r["kern_ms"], r["alg_bytes"], r["schedule"], r["plain"]
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profile(n, L, UNMASK_KERNEL, schedule)
+    traffic = traffic_from_profile(r["n"], L, UNMASK_KERNEL, schedule)
+    mismatches, st = r["mismatches"], r["status"]
+    if cfg5 is not None and mismatches is not None:
+        mismatches += cfg5["verify"]["byte_mismatches"] or 0
+        st |= cfg5["verify"]["status_word"]
 
-    out = None
     if rank == 0:
         cpu = None
         if a.cpu_seconds > 0 and world == 1:
             thr = a.cpu_threads or effective_cores()
             cpu = cpu_baseline(a.cpu_seconds, thr, L, a.seed)
+        job = r["job"]
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -714,27 +904,29 @@ def main():
                                     "device-resident in-place unmask" % job) if job_frames else
                                    "cfg2: 1 GPU device-resident in-place unmask of masked binary frames "
                                    "(aligned arena); N GPUs = per-GPU frame partition",
-                       "frames_per_gpu": g_hi - g_lo, "frame_len": L, "total_frames": job,
-                       "resident_batch_frames": n, "sub_batches": nb,
+                       "frames_per_gpu": r["g_hi"] - r["g_lo"], "frame_len": L, "total_frames": job,
+                       "resident_batch_frames": r["n"], "sub_batches": r["nb"],
                        "layout": "aligned arena, frame i at i*frame_len",
                        "parallelism": f"frame-partition x{world} (no collective)",
                        "dist_backend": a.dist_backend if world > 1 else None,
                        "unmask_schedule": schedule, "unmask_schedule_name": schedule_name(schedule),
-                       "placement": placement},
+                       "placement": r["placement"]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          # the headline itself when the batch is a plain allocation (the default)
                          "frac_plain": (plain["same_schedule"]["frac"] if plain else
-                                        round(achieved / HBM_PEAK_GBS, 4) if arena_used is None else None),
+                                        round(achieved / HBM_PEAK_GBS, 4) if not r["arena_used"] else None),
                          "traffic": traffic,
                          "kernel": UNMASK_KERNEL,
                          "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes},
             "plain_allocation": plain,
-            "hbm_frac_whole_step": round(total_payload / world * (2 + DESC_BYTES / L) /
-                                         (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "hbm_frac_whole_step": round(job * L / world * (2 + DESC_BYTES / L) /
+                                         (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "verify": {"status_word": st, "byte_mismatches": mismatches},
-            "ranks": per_rank,
+            "ranks": r["ranks"],
+            "cfg5_job": cfg5,
+            "e2e_host": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -75,6 +75,20 @@ kmws_status kmws_resident_enable(int device, int on);
 kmws_status kmws_resident_info(int device, uint64_t* jobs, uint64_t* launches, int* running);
 kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_claimed, uint64_t* timeouts,
                                    uint64_t* withdrawn);
+/* Slot ownership guard: posts refused because the calling
+ * thread did not hold the slot (never expected: 0), jobs asked for by a
+ * thread after its exit hook gave its slots back (they launched), and slot
+ * releases that first waited for the slot's last job (an async submit still
+ * running when its thread exited or switched the worker off). */
+kmws_status kmws_resident_guard_counters(int device, uint64_t* unowned_posts, uint64_t* late_posts,
+                                         uint64_t* drained_releases);
+/* Device selection (kmws_gpu.h KMWS_DEVICE_POLICY_*) as a pure function, for
+ * tests: the device `policy` gives a thread on NUMA node `thread_node` (-1:
+ * unknown) when the GPUs' nodes are gpu_nodes[0..ngpus) and `seq` threads
+ * were placed before it on the same candidates. */
+int kmws_device_policy_pick(int policy, int thread_node, const int* gpu_nodes, int ngpus, uint32_t seq);
+/* NUMA node of a gfx950 device's PCIe function (sysfs; -1 unknown). */
+kmws_status kmws_device_numa_node(int device, int* node);
 /* Diagnostics: the worker's workgroup exits so far by reason, counts[0..n):
  * 0 its 1 ms lease ran out, 1 another workgroup found the grid idle, 2 a thread
  * claimed a slot outside the running incarnation (resize), 3 it found the grid

@@ -57,6 +57,38 @@ typedef int kmws_status;
 #define KMWS_RESIDENT_MAX_PAYLOADS 128
 #define KMWS_RESIDENT_MAX_BYTES (256u << 10)
 
+/* ---- device selection (SURVEY 8 e): which GPU a loop thread's objects use ----
+ * kuma runs a pool of event-loop threads (test/client/main.cpp:20,
+ * test/server/main.cpp:22) and every connection's bytes arrive on its loop
+ * thread (TcpConnection.cpp:229).  Every `device` argument below also accepts
+ * KMWS_DEVICE_AUTO: the calling thread's device, kmws_thread_device() -- the
+ * one kmws_set_thread_device pinned, else chosen once for the thread by the
+ * process's policy: NUMA (default: round robin over the GPUs on the NUMA node
+ * of the CPU the thread runs on, over all GPUs when that node has none),
+ * ROUND_ROBIN (over all GPUs, in the order threads first ask), FIRST (device
+ * 0).  So each loop thread's payloads cross its own GPU's PCIe link into its
+ * own pinned staging; host DRAM is what the threads still share.  A thread's
+ * device does not change once chosen.  The library reads no environment. */
+#define KMWS_DEVICE_AUTO (-1)
+enum kmws_device_policy { KMWS_DEVICE_POLICY_NUMA = 0, KMWS_DEVICE_POLICY_ROUND_ROBIN = 1,
+                          KMWS_DEVICE_POLICY_FIRST = 2 };
+kmws_status kmws_set_device_policy(int policy);  /* process-wide; threads that chose keep their device */
+/* Pins the calling thread to `device` (KMWS_DEVICE_AUTO: back to the policy for
+ * objects created later).  KMWS_ERR_NOT_SUPPORTED: no such gfx950 device. */
+kmws_status kmws_set_thread_device(int device);
+/* The calling thread's device (>= 0), or KMWS_ERR_NOT_SUPPORTED without a
+ * gfx950 device. */
+int         kmws_thread_device(void);
+/* Claims the calling thread's slot of `device`'s resident grid now (the
+ * synchronous entries and batch submits otherwise claim it at their first
+ * job) and registers the thread-exit hook that gives it back -- after every
+ * thread_local object constructed before this call returned, i.e. after a
+ * thread_local loop object whose constructor calls it (kmws::RxLoop, TxLoop),
+ * so that object's destructor still flushes on the slot.  A job asked for
+ * after the hook ran launches instead.  Returns the slot, or negative: no
+ * slot free (jobs launch), the worker is off for this thread, or no device. */
+int         kmws_thread_attach(int device);
+
 /* ---- codec results: WSError (src/ws/wsdefs.h:56-67) ---- */
 enum kmws_ws_error {
     KMWS_WS_NOERR = 0, KMWS_WS_NEED_MORE_DATA = 1, KMWS_WS_HANDSHAKE = 2,

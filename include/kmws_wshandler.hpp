@@ -96,9 +96,17 @@ public:
 
     // async: submit at the end of an iteration, deliver at the next ones (the
     // default); false: one synchronous flush per iteration.
-    explicit RxLoop(Poster post, int device = 0, bool async = true)
-        : post_(std::move(post)), batch_(kmws_rx_batch_create(device)), async_(async), alive_(std::make_shared<bool>(true))
+    // device: KMWS_DEVICE_AUTO (the default) = the constructing thread's GPU
+    // (kmws_thread_device: pinned, or its NUMA node's), so construct the loop
+    // on its event-loop thread.  attach: claim that thread's resident slot now
+    // (kmws_thread_attach) -- for a loop that is a thread_local of its own loop
+    // thread (forThisThread): the thread then gives the slot back only after
+    // this loop's destructor has flushed on it.
+    explicit RxLoop(Poster post, int device = KMWS_DEVICE_AUTO, bool async = true, bool attach = false)
+        : post_(std::move(post)), device_(device == KMWS_DEVICE_AUTO ? kmws_thread_device() : device),
+          batch_(kmws_rx_batch_create(device_)), async_(async), alive_(std::make_shared<bool>(true))
     {
+        if (batch_ && attach) (void)kmws_thread_attach(device_);
     }
     ~RxLoop()
     {
@@ -112,13 +120,14 @@ public:
     RxLoop& operator=(const RxLoop&) = delete;
 
     // The RxLoop of the calling (event-loop) thread, created on first use.
-    static RxLoop& forThisThread(Poster post, int device = 0)
+    static RxLoop& forThisThread(Poster post, int device = KMWS_DEVICE_AUTO)
     {
-        thread_local RxLoop loop(std::move(post), device);
+        thread_local RxLoop loop(std::move(post), device, true, true);
         return loop;
     }
 
     bool valid() const { return batch_ != nullptr; }
+    int device() const { return device_; }
     kmws_rx_batch* batch() const { return batch_; }
     // (Re)binds the loop's post function (e.g. when the loop object is created
     // before its event loop runs).
@@ -198,6 +207,7 @@ public:
 
 private:
     Poster post_;
+    int device_;
     kmws_rx_batch* batch_;
     bool async_;
     bool armed_ = false;
@@ -253,12 +263,18 @@ public:
     // ring_bytes: the pinned send ring (a small one stays in the CPU's caches:
     // the payload copies and the socket writes hit it); a payload that does
     // not fit goes through a buffer of its own
-    explicit TxLoop(Poster post, int device = 0, size_t ring_bytes = (size_t)1 << 20, int max_inflight = 1)
-        : post_(std::move(post)), batch_(kmws_tx_batch_create(device)), max_inflight_(max_inflight < 1 ? 1 : max_inflight),
+    // device, attach: as RxLoop's (KMWS_DEVICE_AUTO: the constructing thread's
+    // GPU; attach: its resident slot claimed now, given back after this loop's
+    // destructor -- forThisThread does)
+    explicit TxLoop(Poster post, int device = KMWS_DEVICE_AUTO, size_t ring_bytes = (size_t)1 << 20,
+                    int max_inflight = 1, bool attach = false)
+        : post_(std::move(post)), device_(device == KMWS_DEVICE_AUTO ? kmws_thread_device() : device),
+          batch_(kmws_tx_batch_create(device_)), max_inflight_(max_inflight < 1 ? 1 : max_inflight),
           alive_(std::make_shared<bool>(true))
     {
         if (!batch_) return;
-        ring_ = static_cast<uint8_t*>(kmws_host_alloc(ring_bytes, device));
+        if (attach) (void)kmws_thread_attach(device_);
+        ring_ = static_cast<uint8_t*>(kmws_host_alloc(ring_bytes, device_));
         if (ring_ && kmws_tx_batch_attach_ring(batch_, ring_, ring_bytes) == KMWS_OK) {
             ring_bytes_ = ring_bytes;
         } else {
@@ -273,19 +289,27 @@ public:
             (void)flush();  // every queued frame is written: close connections first
             kmws_tx_batch_destroy(batch_);
         }
-        kmws_host_free(ring_);
+        // after a mask that timed out the device may still write the ring: it
+        // is never freed (nor reused)
+        if (broken_ != KMWS_ERR_TIMEOUT) kmws_host_free(ring_);
     }
     TxLoop(const TxLoop&) = delete;
     TxLoop& operator=(const TxLoop&) = delete;
 
     // The TxLoop of the calling (event-loop) thread, created on first use.
-    static TxLoop& forThisThread(Poster post, int device = 0)
+    static TxLoop& forThisThread(Poster post, int device = KMWS_DEVICE_AUTO)
     {
-        thread_local TxLoop loop(std::move(post), device);
+        thread_local TxLoop loop(std::move(post), device, (size_t)1 << 20, 1, true);
         return loop;
     }
 
-    bool valid() const { return batch_ != nullptr && ring_ != nullptr; }
+    bool valid() const { return batch_ != nullptr && ring_ != nullptr && broken_ == 0; }
+    int device() const { return device_; }
+    // Frames dropped because their generation's mask failed (never written;
+    // their connections' lastResult() says why).  A mask that timed out
+    // (KMWS_ERR_TIMEOUT) also retires the loop: later sends return it.
+    uint64_t dropped() const { return dropped_; }
+    int broken() const { return broken_; }
     // A new poster holds none of this loop's tasks: the next arm() posts again
     // (a task left with the old one never ran, or runs as a harmless extra pass).
     void setPoster(Poster post)
@@ -345,6 +369,7 @@ public:
     // KMWS_ERR_BUFFER_TOO_LONG and send nothing (as kuma, :427).
     int sendChain(Conn* c, const kmws_frame_hdr& hdr, const uint8_t* const* segs, const size_t* lens, size_t nseg)
     {
+        if (broken_) return broken_;
         if (!valid() || !c) return KMWS_ERR_INVALID_STATE;
         size_t plen = 0, nonempty = 0;
         for (size_t i = 0; i < nseg; ++i) {
@@ -380,7 +405,7 @@ public:
             if (r < 0) return r;
         }
         uint8_t* p = place(plen, &f);
-        if (!p) return KMWS_ERR_FAILED;
+        if (!p) return broken_ ? broken_ : KMWS_ERR_FAILED;
         for (size_t i = 0, pos = 0; i < nseg; pos += lens[i], ++i)
             if (lens[i]) std::memcpy(p + pos, segs[i], lens[i]);
         f.payload = p;
@@ -460,6 +485,7 @@ private:
         uint64_t bytes = 0;    // their bytes
         int64_t ticket = 0;
         size_t ring_used = 0;  // ring bytes (with alignment and wrap waste) freed when written
+        bool dropped = false;  // its mask failed: never written
     };
 
     // Room for n payload bytes: 16-byte aligned in the ring, after the bytes
@@ -497,7 +523,16 @@ private:
         if (cur_.frames.empty()) return 0;
         if (cur_.masked) {
             const int64_t t = kmws_tx_batch_submit(batch_);
-            if (t < 0) return (int)t;
+            if (t <= 0) {
+                // the batch dropped the generation's masks (nothing runs on
+                // them): its frames are never written -- their payloads are not
+                // masked although their headers say so
+                const int st = t < 0 ? (int)t : KMWS_ERR_FAILED;
+                drop(cur_, st);
+                used_ -= cur_.ring_used;  // the newest ring bytes: nothing writes them
+                cur_ = Gen();
+                return st;
+            }
             cur_.ticket = t;
         }
         inflight_.push_back(std::move(cur_));
@@ -514,13 +549,11 @@ private:
             Gen& g = inflight_.front();
             if (g.ticket > 0) {
                 const int p = kmws_tx_batch_poll(batch_, g.ticket, wait ? 1 : 0);
-                if (p < 0) return p;
+                if (p < 0) return failOldest(p);
                 if (p == 0) break;
             }
             n += write(g);
-            used_ -= g.ring_used;
-            tail_ = (tail_ + g.ring_used) % ring_bytes_;
-            inflight_.pop_front();
+            retireOldest();
         }
         if (inflight_.empty() && cur_.frames.empty() && cur_.ring_used == 0) tail_ = used_ = 0;
         return n;
@@ -530,13 +563,53 @@ private:
         Gen& g = inflight_.front();
         if (g.ticket > 0) {
             const int p = kmws_tx_batch_poll(batch_, g.ticket, 1);
-            if (p < 0) return p;
+            if (p < 0) return failOldest(p);
         }
         const int n = write(g);
+        retireOldest();
+        return n;
+    }
+    void retireOldest()
+    {
+        Gen& g = inflight_.front();
         used_ -= g.ring_used;
         tail_ = (tail_ + g.ring_used) % ring_bytes_;
         inflight_.pop_front();
-        return n;
+    }
+    // The oldest generation's mask failed (the batch has retired it): its
+    // frames are dropped, not written.  KMWS_ERR_TIMEOUT: the device may still
+    // write its ring bytes -- the loop is retired (later generations written
+    // if their masks finish, frames not yet submitted dropped, the ring never
+    // reused or freed); any other failure frees them.
+    int failOldest(int st)
+    {
+        drop(inflight_.front(), st);
+        if (st != KMWS_ERR_TIMEOUT) {
+            retireOldest();
+            return st;
+        }
+        broken_ = st;
+        inflight_.pop_front();  // its ring bytes stay allocated: the ring is never reused
+        while (!inflight_.empty()) {  // later generations: written if their masks finish
+            Gen& g = inflight_.front();
+            const int p = g.ticket > 0 ? kmws_tx_batch_poll(batch_, g.ticket, 1) : 1;
+            if (p == 1) (void)write(g);
+            else drop(g, p < 0 ? p : st);
+            inflight_.pop_front();
+        }
+        drop(cur_, st);
+        cur_ = Gen();
+        return st;
+    }
+    void drop(Gen& g, int st)
+    {
+        if (g.dropped) return;
+        g.dropped = true;
+        for (Frame& f : g.frames) {
+            --f.conn->queued_;
+            f.conn->last_ = st;
+        }
+        dropped_ += g.frames.size();
     }
 
     // Each connection's consecutive frames of the generation as one writev
@@ -563,6 +636,7 @@ private:
     }
 
     Poster post_;
+    int device_;
     kmws_tx_batch* batch_;
     int max_inflight_;
     std::shared_ptr<bool> alive_;
@@ -574,6 +648,8 @@ private:
     std::vector<std::unique_ptr<Conn>> conns_;
     bool armed_ = false;
     int last_ = 0;
+    int broken_ = 0;         // KMWS_ERR_TIMEOUT once a mask timed out
+    uint64_t dropped_ = 0;
 };
 
 template <class FrameHeader, class Buffer, class WSError, class WSMode, class CbResult>
@@ -581,7 +657,9 @@ class BasicWSHandler {
 public:
     using FrameCallback = std::function<CbResult(FrameHeader, Buffer&)>;  // WSHandler.h:35
 
-    explicit BasicWSHandler(int device = 0) : st_(std::make_shared<State>(device)) {}
+    // device: KMWS_DEVICE_AUTO (the default) = the constructing thread's GPU;
+    // kuma creates a connection's handler on its loop thread
+    explicit BasicWSHandler(int device = KMWS_DEVICE_AUTO) : st_(std::make_shared<State>(device)) {}
     ~BasicWSHandler()
     {
         if (st_) {
@@ -650,7 +728,7 @@ public:
 
     // WSHandler::handleDataMask(key, data, len) (WSHandler.cpp:303-310), on the GPU
     static kmws_status handleDataMask(const uint8_t mask_key[KMWS_MASK_KEY_SIZE], uint8_t* data, size_t len,
-                                      int device = 0)
+                                      int device = KMWS_DEVICE_AUTO)
     {
         if (data == nullptr || len == 0) return KMWS_OK;  // :305
         uint8_t* segs[1] = {data};
@@ -660,7 +738,8 @@ public:
 
     // WSHandler::handleDataMask(key, KMBuffer&) (WSHandler.cpp:312-322): the key
     // phase continues across the chain's segments; on the GPU, one launch
-    static kmws_status handleDataMask(const uint8_t mask_key[KMWS_MASK_KEY_SIZE], Buffer& buf, int device = 0)
+    static kmws_status handleDataMask(const uint8_t mask_key[KMWS_MASK_KEY_SIZE], Buffer& buf,
+                                      int device = KMWS_DEVICE_AUTO)
     {
         std::vector<uint8_t*> segs;
         std::vector<size_t> lens;

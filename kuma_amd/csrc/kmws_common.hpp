@@ -97,6 +97,10 @@ inline uint64_t piece_count(uint64_t off, uint32_t len)
 kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const PieceRec* pieces, uint32_t np,
                                  hipStream_t s);
 
+// KMWS_DEVICE_AUTO -> the calling thread's device (kmws_devmap.cpp; negative
+// without a gfx950 device); any other value unchanged.
+int resolve_device(int device);
+
 // Resident worker (kmws_resident.hip): host jobs of at most kResMaxDescs
 // payloads and kResMaxBytes bytes go to the calling thread's slot of a grid
 // that stays on the GPU polling pinned memory, instead of a launch per call.

@@ -161,11 +161,20 @@ namespace {
 class StagePool;
 StagePool& stage_pool();
 
-struct HotStage {  // the calling thread's kept stage
-    PinnedStage* s = nullptr;
-    ~HotStage();
+// The calling thread's kept stage.  Plain data (zero-initialised, trivially
+// destructible), so a call from another thread_local object's destructor after
+// the thread's exit hook ran still finds it valid: such a call gives its stage
+// to the pool instead of keeping it (which would leak it with the thread).
+struct HotStage {
+    PinnedStage* s;
+    bool gone;  // the thread's exit hook ran
 };
 thread_local HotStage t_hot;
+struct HotStageExit {  // returns the kept stage to the pool at thread exit
+    bool armed = false;
+    ~HotStageExit();
+};
+thread_local HotStageExit t_hot_exit;
 
 class StagePool {
 public:
@@ -202,7 +211,8 @@ public:
     void give(PinnedStage* s, bool keep = true)
     {
         s->clear();
-        if (keep && !t_hot.s) {
+        if (keep && !t_hot.s && !t_hot.gone) {
+            t_hot_exit.armed = true;  // constructed before the stage is kept: it gives it back
             t_hot.s = s;
             return;
         }
@@ -221,9 +231,13 @@ StagePool& stage_pool()
     return *p;
 }
 
-HotStage::~HotStage()
+HotStageExit::~HotStageExit()
 {
-    if (s) stage_pool().give(s, false);
+    t_hot.gone = true;
+    if (PinnedStage* s = t_hot.s) {
+        t_hot.s = nullptr;
+        stage_pool().give(s, false);
+    }
 }
 
 // A stage borrowed for the scope of one call (taken at first use).
@@ -406,7 +420,7 @@ kmws_decoder* kmws_decoder_create(int mode, int device)
     kmws_decoder* d = new (std::nothrow) kmws_decoder();
     if (d) {
         d->mode = mode;
-        d->device = device;
+        d->device = resolve_device(device);  // KMWS_DEVICE_AUTO: the creating (loop) thread's GPU
     }
     return d;
 }
@@ -547,6 +561,10 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
     }
     if (total == 0) return KMWS_OK;  // nothing to do (:305)
     if (total > 0xFFFFFFFFull) return KMWS_ERR_INVALID_PARAM;
+    if (device == KMWS_DEVICE_AUTO) {
+        device = kmws_thread_device();
+        if (device < 0) return device;
+    }
     if (device < 0) return KMWS_ERR_INVALID_PARAM;
     BorrowedStage bs(device);  // a stage of the process's pool for this call (StagePool)
     PinnedStage* s = bs.get();
@@ -577,6 +595,7 @@ kmws_status kmws_mask_host_chain(const uint8_t key[KMWS_MASK_KEY_SIZE], uint8_t*
 
 void* kmws_host_alloc(size_t bytes, int device)
 {
+    device = resolve_device(device);
     if (bytes == 0 || device < 0 || kmws_device_count() <= device) return nullptr;
     DevGuard g(device);
     void* p = nullptr;
@@ -662,6 +681,7 @@ struct kmws_tx_batch {
 
 kmws_tx_batch* kmws_tx_batch_create(int device)
 {
+    device = resolve_device(device);
     kmws_tx_batch* b = new (std::nothrow) kmws_tx_batch();
     if (!b) return nullptr;
     if (b->prepare(device) != KMWS_OK) {
@@ -844,6 +864,7 @@ int64_t kmws_tx_batch_flush(kmws_tx_batch* b)
 
 kmws_rx_batch* kmws_rx_batch_create(int device)
 {
+    device = resolve_device(device);
     kmws_rx_batch* b = new (std::nothrow) kmws_rx_batch();
     if (!b) return nullptr;
     if (b->prepare(device) != KMWS_OK) {

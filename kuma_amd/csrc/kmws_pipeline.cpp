@@ -67,6 +67,7 @@ extern "C" {
 
 kmws_pipeline* kmws_pipeline_create(int device, uint64_t chunk_bytes, uint32_t max_frames_per_chunk, int depth)
 {
+    device = resolve_device(device);
     if (device < 0 || device >= kmws_device_count() || chunk_bytes < 4096 || depth < 1 || depth > 8 ||
         max_frames_per_chunk == 0)
         return nullptr;

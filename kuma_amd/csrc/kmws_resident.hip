@@ -459,8 +459,9 @@ class ResidentWorker {
 public:
     explicit ResidentWorker(int device) : device_(device) {}
 
-    // A free slot for the calling thread, or -1 (all taken, or unusable).
-    int claim()
+    // A free slot for the calling thread (its owner token `me`, never 0), or
+    // -1 (all taken, or unusable).
+    int claim(uint64_t me)
     {
         if (!usable()) return -1;
         uint32_t m = ld_acq(&claimed_);
@@ -468,6 +469,7 @@ public:
             if (m == 0xFFFFFFFFu >> (32 - kResSlots)) return -1;
             const int b = __builtin_ctz(~m);
             if (__atomic_compare_exchange_n(&claimed_, &m, m | (1u << b), false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                __atomic_store_n(&hs_[b].owner, me, __ATOMIC_RELEASE);
                 // the workgroup polls the descriptors from now on (no job: same number)
                 __atomic_fetch_or(&mb_->slot[b].word, kClaimedBit, __ATOMIC_RELEASE);
                 // a running incarnation without this slot's workgroups is asked
@@ -478,15 +480,31 @@ public:
             }
         }
     }
-    // The thread gives its slot back (thread exit, or it switched the worker
-    // off).  A job still posted on it stays posted and is served.
-    void release(int b)
+    // The thread `me` gives slot b back (thread exit, or it switched the worker
+    // off).  Its last job -- an rx / tx batch's submit may still be running --
+    // is first waited for: finished (its batch's poll then sees it done), or
+    // withdrawn unrun (the poll sees that and launches it).  Only then may
+    // another thread claim the slot and post on it: a job number the slot's
+    // next holder reuses can no longer be mistaken for this thread's.  False:
+    // the job neither finished nor left in time -- the slot stays taken.
+    bool release(int b, uint64_t me)
     {
-        if (b < 0 || b >= kResSlots || !mb_) return;
+        if (b < 0 || b >= kResSlots || !mb_) return true;
+        if (__atomic_load_n(&hs_[b].owner, __ATOMIC_ACQUIRE) != me) return true;  // not this thread's
+        const uint64_t s = hs_[b].seq;
+        if (s && hs_[b].cancelled != s && !all_done(mb_->slot[b], s, hs_[b].parts)) {
+            __atomic_fetch_add(&drained_, 1, __ATOMIC_RELAXED);
+            if (wait(b, s) == KMWS_ERR_TIMEOUT) return false;
+        }
+        __atomic_store_n(&hs_[b].owner, 0ull, __ATOMIC_RELEASE);
         if (!__atomic_load_n(&exiting_, __ATOMIC_ACQUIRE))
             __atomic_fetch_and(&mb_->slot[b].word, ~kClaimedBit, __ATOMIC_RELEASE);
         __atomic_fetch_and(&claimed_, ~(1u << b), __ATOMIC_ACQ_REL);
+        return true;
     }
+    // A thread whose slots were given back at its exit asked for a job: it
+    // launches instead (counted).
+    void note_late_post() { __atomic_fetch_add(&late_posts_, 1, __ATOMIC_RELAXED); }
 
     // Ask every workgroup to leave at its next poll and wait for the grid (atexit).
     void quit_and_wait()
@@ -518,11 +536,17 @@ public:
     // calling thread) and returns without waiting; *job = its number.
     // KMWS_ERR_NOT_SUPPORTED: the slot's previous job is still running, or the
     // worker cannot be (re)launched -- nothing was posted.
-    kmws_status post(int b, const ResDesc* d, uint32_t n, uint64_t* job)
+    kmws_status post(int b, uint64_t me, const ResDesc* d, uint32_t n, uint64_t* job)
     {
         if (n == 0 || n > (uint32_t)kResMaxDescs || !usable()) return KMWS_ERR_NOT_SUPPORTED;
         for (uint32_t i = 0; i < n; ++i)
             if ((d[i].addr >> 48) != 0 || d[i].len > kLenMask) return KMWS_ERR_NOT_SUPPORTED;
+        // only the slot's holder writes its descriptors and job word: a post
+        // from any other thread is refused (and counted -- never expected)
+        if (__atomic_load_n(&hs_[b].owner, __ATOMIC_ACQUIRE) != me) {
+            __atomic_fetch_add(&unowned_posts_, 1, __ATOMIC_RELAXED);
+            return KMWS_ERR_NOT_SUPPORTED;
+        }
         ResSlot& sl = mb_->slot[b];
         const uint64_t prev = hs_[b].seq;
         uint64_t cur = ld_acq(&inc_);
@@ -551,8 +575,8 @@ public:
             __atomic_store_n(q, x.addr, __ATOMIC_RELAXED);
             __atomic_store_n(q + 1, (uint64_t)x.len | (uint64_t)x.key << 32, __ATOMIC_RELAXED);
         }
-        hs_[b].seq = s;
-        hs_[b].parts = parts;
+        __atomic_store_n(&hs_[b].parts, parts, __ATOMIC_RELAXED);
+        __atomic_store_n(&hs_[b].seq, s, __ATOMIC_RELEASE);
         __atomic_store_n(&hs_[b].jobs, hs_[b].jobs + 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
         __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | (uint64_t)(parts - 1) << kPartShift | kClaimedBit,
                          __ATOMIC_RELEASE);
@@ -566,6 +590,7 @@ public:
     int test(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
+        if (withdrawn_job(b, s)) return KMWS_ERR_NOT_SUPPORTED;
         if (finished(b, s)) return 1;
         const uint64_t cur = ld_acq(&inc_);
         if (ld_acq(&mb_->exited) == cur) {
@@ -583,6 +608,7 @@ public:
     kmws_status wait(int b, uint64_t s)
     {
         ResSlot& sl = mb_->slot[b];
+        if (withdrawn_job(b, s)) return KMWS_ERR_NOT_SUPPORTED;  // (by its thread's release at exit)
         const auto t0 = Clock::now();
         Clock::time_point orphan{};
         for (uint32_t spin = 0;; ++spin) {
@@ -619,6 +645,9 @@ public:
     uint64_t launches() const { return ld_acq(&inc_); }
     uint64_t timeouts() const { return ld_acq(&timeouts_); }
     uint64_t withdrawn() const { return ld_acq(&withdrawn_); }
+    uint64_t unowned_posts() const { return ld_acq(&unowned_posts_); }
+    uint64_t late_posts() const { return ld_acq(&late_posts_); }
+    uint64_t drained() const { return ld_acq(&drained_); }
     int claimed() const { return __builtin_popcount(ld_acq(&claimed_)); }
     // Workgroup exits so far by reason (ResCtl::why), read from device memory.
     kmws_status exit_reasons(uint64_t* out, int n)
@@ -652,7 +681,15 @@ private:
     }
     // Job s of slot b finished -- or the slot has moved on (a later job is
     // posted only once s was finished or withdrawn, by s's own waiter).
-    bool finished(int b, uint64_t s) const { return hs_[b].seq != s || all_done(mb_->slot[b], s, hs_[b].parts); }
+    // (Read by the job's poller, which after a release at thread exit may not
+    // be the slot's holder any more: atomic loads.)
+    bool finished(int b, uint64_t s) const
+    {
+        return ld_acq(&hs_[b].seq) != s || all_done(mb_->slot[b], s, ld_acq(&hs_[b].parts));
+    }
+    // Job s of slot b was withdrawn unrun (by its waiter, or by the release at
+    // its thread's exit): its caller launches it.
+    bool withdrawn_job(int b, uint64_t s) const { return ld_acq(&hs_[b].cancelled) == s; }
     // Has the workgroup of an unfinished part of job s left grid `cur`?
     static bool part_left(const ResSlot& sl, uint64_t s, uint32_t parts, uint64_t cur)
     {
@@ -679,7 +716,7 @@ private:
             if (!all_left && ld_acq(&sl.gone[j]) != cur) return false;
         }
         __atomic_store_n(&sl.word, (ld_acq(&sl.word) | kCancelBit) & ~kQuitBit, __ATOMIC_RELEASE);
-        hs_[b].cancelled = s;
+        __atomic_store_n(&hs_[b].cancelled, s, __ATOMIC_RELEASE);
         __atomic_fetch_add(&withdrawn_, 1, __ATOMIC_RELAXED);
         __atomic_store_n(&hs_[b].jobs, hs_[b].jobs - 1, __ATOMIC_RELAXED);
         return true;
@@ -748,10 +785,6 @@ private:
                 return KMWS_ERR_FAILED;
             }
         }
-        if (hipMemset(dctl_, 0, sizeof(ResCtl)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            (void)hipGetLastError();
-            return KMWS_ERR_FAILED;
-        }
         // A non-blocking stream: the legacy default stream (torch's current stream
         // unless the caller picked another) waits for every blocking stream's
         // work, which would include this kernel -- measured: a kernel on the null
@@ -766,6 +799,14 @@ private:
             greatest = least = 0;
         }
         if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest) != hipSuccess) {
+            (void)hipGetLastError();
+            return KMWS_ERR_FAILED;
+        }
+        // cleared on the worker's own stream: a device-wide synchronize here
+        // would wait for every stream of the process (a long kernel elsewhere),
+        // with launch_mu_ held
+        if (hipMemsetAsync(dctl_, 0, sizeof(ResCtl), stream_) != hipSuccess ||
+            hipStreamSynchronize(stream_) != hipSuccess) {
             (void)hipGetLastError();
             return KMWS_ERR_FAILED;
         }
@@ -837,11 +878,15 @@ private:
         uint64_t seq = 0;        // last job number posted
         uint64_t cancelled = 0;  // the last job withdrawn
         uint64_t jobs = 0;       // jobs posted and not withdrawn (summed by jobs())
+        uint64_t owner = 0;      // owner token of the thread holding the slot (0: free)
         uint32_t parts = 0;      // parts of job `seq`
     };
     SlotHost hs_[kResSlots];
     alignas(64) uint64_t timeouts_ = 0;
     uint64_t withdrawn_ = 0;
+    uint64_t unowned_posts_ = 0;  // posts refused: the caller did not hold the slot
+    uint64_t late_posts_ = 0;     // jobs asked for after the thread gave its slots back (launched)
+    uint64_t drained_ = 0;        // releases that first waited for the slot's last job
 };
 
 // Every worker of the process (for the exit handler); never freed.
@@ -875,22 +920,43 @@ ResidentWorker* worker(int device)
     return w;
 }
 
-// The calling thread's slots, one per device (-1: none held; -2: its job
-// timed out, the slot is never given back), released when the thread exits.
-// kmws_resident_enable(0) makes the thread's calls launch instead (the A/B of
-// the worker) and gives its slot back.
+// The calling thread's slots, one per device.  Plain data -- zero-initialised,
+// trivially destructible -- so it stays valid while the thread's other
+// thread_local objects are destroyed, before and after ThreadExit below gives
+// the slots back.  slot1[d] = slot + 1 (0: none held; -1: its job timed out,
+// the slot is never given back).  kmws_resident_enable(0) makes the thread's
+// calls launch instead (the A/B of the worker) and gives its slot back.
 struct ThreadSlots {
-    int8_t slot[kMaxDevices];
-    uint64_t off_mask = 0;  // bit d: worker off for device d on this thread
-    ThreadSlots() { std::memset(slot, -1, sizeof slot); }
-    ~ThreadSlots()
-    {
-        for (int d = 0; d < kMaxDevices; ++d)
-            if (slot[d] >= 0)
-                if (ResidentWorker* w = __atomic_load_n(&g_by_dev[d], __ATOMIC_ACQUIRE)) w->release(slot[d]);
-    }
+    int8_t slot1[kMaxDevices];
+    uint64_t off_mask;  // bit d: worker off for device d on this thread
+    uint64_t token;     // this thread's owner token (0 until its first claim)
+    bool gone;          // its slots were given back at thread exit: later jobs launch
 };
 thread_local ThreadSlots t_slots;
+
+// Gives the thread's slots back when it exits.  Constructed at the thread's
+// first claim (or by kmws_thread_attach), so C++'s reverse order of
+// thread_local destruction runs it after every thread_local object that was
+// complete by then -- and before those completed later.  VERDICT r05: a
+// thread_local RxLoop / TxLoop made before the thread's first job was
+// destroyed AFTER the slot had been given back, and its flush posted on a slot
+// another thread might hold by then (both wrote the same job number).  Now
+// such a flush finds `gone` set and launches; a loop that attached in its
+// constructor is destroyed first and flushes on its slot.
+struct ThreadExit {
+    bool armed = false;
+    ~ThreadExit()
+    {
+        t_slots.gone = true;
+        for (int d = 0; d < kMaxDevices; ++d)
+            if (t_slots.slot1[d] > 0)
+                if (ResidentWorker* w = __atomic_load_n(&g_by_dev[d], __ATOMIC_ACQUIRE))
+                    t_slots.slot1[d] = w->release(t_slots.slot1[d] - 1, t_slots.token) ? 0 : -1;
+    }
+};
+thread_local ThreadExit t_exit;
+
+uint64_t g_next_token = 0;
 
 // The calling thread's slot on `device` (claimed on first use), or -1.
 int thread_slot(int device, ResidentWorker** wout)
@@ -899,11 +965,16 @@ int thread_slot(int device, ResidentWorker** wout)
     ResidentWorker* w = worker(device);
     if (!w) return -1;
     *wout = w;
-    int b = t_slots.slot[device];
-    if (b == -1) {
-        b = w->claim();
-        if (b >= 0) t_slots.slot[device] = (int8_t)b;
+    if (t_slots.gone) {  // past this thread's ThreadExit: nothing is claimed any more
+        w->note_late_post();
+        return -1;
     }
+    const int s1 = t_slots.slot1[device];
+    if (s1 != 0) return s1 - 1;  // held (or -2: kept by a timed-out job)
+    if (!t_slots.token) t_slots.token = __atomic_add_fetch(&g_next_token, 1, __ATOMIC_RELAXED);
+    t_exit.armed = true;  // constructs it before the claim: the slot is given back at exit
+    const int b = w->claim(t_slots.token);
+    if (b >= 0) t_slots.slot1[device] = (int8_t)(b + 1);
     return b;
 }
 
@@ -933,7 +1004,7 @@ kmws_status resident_post(int device, const kmws_desc* descs, const uint8_t* dev
     }
     if (bytes > max_bytes || bytes > kResMaxBytesAsync) return KMWS_ERR_NOT_SUPPORTED;
     uint64_t s = 0;
-    const kmws_status st = w->post(b, d, (uint32_t)k, &s);
+    const kmws_status st = w->post(b, t_slots.token, d, (uint32_t)k, &s);
     if (st != KMWS_OK) return st;
     job->device = device;
     job->slot = b;
@@ -953,8 +1024,8 @@ kmws_status resident_wait(const ResidentJob& job)
     if (!w) return KMWS_ERR_INVALID_PARAM;
     const kmws_status st = w->wait(job.slot, job.seq);
     if (st == KMWS_ERR_TIMEOUT && job.device >= 0 && job.device < kMaxDevices &&
-        t_slots.slot[job.device] == job.slot)
-        t_slots.slot[job.device] = -2;  // the slot stays the device's
+        t_slots.slot1[job.device] == job.slot + 1)
+        t_slots.slot1[job.device] = -1;  // the slot stays the device's
     return st;
 }
 
@@ -978,10 +1049,9 @@ kmws_status kmws_resident_enable(int device, int on)
         ts.off_mask &= ~(1ull << device);
     } else {
         ts.off_mask |= 1ull << device;
-        if (ts.slot[device] >= 0) {
-            if (kmws::ResidentWorker* w = __atomic_load_n(&kmws::g_by_dev[device], __ATOMIC_ACQUIRE))
-                w->release(ts.slot[device]);
-            ts.slot[device] = -1;
+        if (ts.slot1[device] > 0) {
+            kmws::ResidentWorker* w = __atomic_load_n(&kmws::g_by_dev[device], __ATOMIC_ACQUIRE);
+            ts.slot1[device] = !w || w->release(ts.slot1[device] - 1, ts.token) ? 0 : -1;
         }
     }
     return KMWS_OK;
@@ -1002,11 +1072,35 @@ kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_clai
 {
     kmws::ResidentWorker* w = kmws::worker(device);
     if (!w) return KMWS_ERR_INVALID_PARAM;
-    if (thread_slot) *thread_slot = kmws::t_slots.slot[device] >= 0 ? kmws::t_slots.slot[device] : -1;
+    if (thread_slot) *thread_slot = kmws::t_slots.slot1[device] > 0 ? kmws::t_slots.slot1[device] - 1 : -1;
     if (slots_claimed) *slots_claimed = w->claimed();
     if (timeouts) *timeouts = w->timeouts();
     if (withdrawn) *withdrawn = w->withdrawn();
     return KMWS_OK;
+}
+
+kmws_status kmws_resident_guard_counters(int device, uint64_t* unowned_posts, uint64_t* late_posts,
+                                         uint64_t* drained_releases)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    if (unowned_posts) *unowned_posts = w->unowned_posts();
+    if (late_posts) *late_posts = w->late_posts();
+    if (drained_releases) *drained_releases = w->drained();
+    return KMWS_OK;
+}
+
+int kmws_thread_attach(int device)
+{
+    if (device == KMWS_DEVICE_AUTO) device = kmws_thread_device();
+    if (device < 0 || device >= kmws::kMaxDevices || kmws_device_count() <= device) return KMWS_ERR_NOT_SUPPORTED;
+    kmws::ResidentWorker* w = nullptr;
+    const int b = kmws::thread_slot(device, &w);
+    // even without a slot (all taken, worker off): the thread's exit hook now
+    // exists, so a slot claimed later is still given back after this caller's
+    // thread_local objects
+    if (!kmws::t_slots.gone) kmws::t_exit.armed = true;
+    return b;
 }
 
 kmws_status kmws_resident_exit_reasons(int device, uint64_t* counts, int n)

@@ -25,6 +25,8 @@ WS_NOERR, WS_NEED_MORE_DATA, WS_INVALID_FRAME, WS_INVALID_LENGTH = 0, 1, 5, 6
 WS_PROTOCOL_ERROR, WS_CLOSED, WS_DESTROYED = 7, 8, 9
 MAX_HEADER_SIZE = 14
 FLAG_MASK = 0x100
+DEVICE_AUTO = -1  # KMWS_DEVICE_AUTO: the calling thread's device
+DEVICE_POLICY_NUMA, DEVICE_POLICY_ROUND_ROBIN, DEVICE_POLICY_FIRST = 0, 1, 2
 
 #: every function include/kmws_gpu.h declares (tests check they are exported)
 EXPORTS = [
@@ -44,12 +46,14 @@ EXPORTS = [
     "kmws_rx_batch_attach_ring",
     "kmws_tx_batch_create", "kmws_tx_batch_destroy", "kmws_tx_batch_add", "kmws_tx_batch_flush",
     "kmws_tx_batch_pending", "kmws_tx_batch_attach_ring", "kmws_host_alloc", "kmws_host_free",
+    "kmws_set_device_policy", "kmws_set_thread_device", "kmws_thread_device", "kmws_thread_attach",
 ]
 #: every function include/kmws_bench.h declares (bench / test support, same library)
 BENCH_EXPORTS = [
     "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
     "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info", "kmws_resident_counters",
-    "kmws_resident_exit_reasons",
+    "kmws_resident_exit_reasons", "kmws_resident_guard_counters", "kmws_device_policy_pick",
+    "kmws_device_numa_node",
 ]
 
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
@@ -175,6 +179,14 @@ def bind(L: C.CDLL) -> C.CDLL:
         "kmws_pipeline_set_transfer": (i32, [vp, i32]),
         "kmws_pipeline_unmask": (i32, [vp, u8p, u64, vp, u32]),
         "kmws_find_headers": (i32, [u8p, u64, vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+        "kmws_set_device_policy": (i32, [i32]),
+        "kmws_set_thread_device": (i32, [i32]),
+        "kmws_thread_device": (i32, []),
+        "kmws_thread_attach": (i32, [i32]),
+        "kmws_resident_guard_counters": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                               C.POINTER(C.c_uint64)]),
+        "kmws_device_policy_pick": (i32, [i32, i32, C.POINTER(C.c_int), i32, u32]),
+        "kmws_device_numa_node": (i32, [i32, C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -347,6 +359,39 @@ def resident_info(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
     return {"jobs": jobs.value, "launches": launches.value, "running": bool(running.value),
             "thread_slot": slot.value, "slots_claimed": claimed.value, "timeouts": tmo.value,
             "withdrawn": wd.value}
+
+
+def resident_guard(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
+    """kmws_resident_guard_counters: posts refused on a slot the caller did not
+    hold (never expected), jobs asked for after a thread's exit hook gave its
+    slots back (launched), releases that first waited for the slot's last job."""
+    L = L or lib()
+    a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+    _check(L.kmws_resident_guard_counters(device, C.byref(a), C.byref(b), C.byref(c)), "kmws_resident_guard_counters")
+    return {"unowned_posts": a.value, "late_posts": b.value, "drained_releases": c.value}
+
+
+def device_policy_pick(policy: int, thread_node: int, gpu_nodes: Sequence[int], seq: int) -> int:
+    """kmws_device_policy_pick: the device `policy` gives a thread on NUMA node
+    `thread_node` (-1 unknown) for GPUs on `gpu_nodes`, after `seq` threads."""
+    arr = (C.c_int * max(1, len(gpu_nodes)))(*gpu_nodes)
+    return lib().kmws_device_policy_pick(policy, thread_node, arr, len(gpu_nodes), seq & 0xFFFFFFFF)
+
+
+def set_device_policy(policy: int) -> None:
+    _check(lib().kmws_set_device_policy(policy), "kmws_set_device_policy")
+
+
+def set_thread_device(device: int) -> None:
+    _check(lib().kmws_set_thread_device(device), "kmws_set_thread_device")
+
+
+def thread_device() -> int:
+    """kmws_thread_device: the calling thread's GPU (raises without one)."""
+    d = lib().kmws_thread_device()
+    if d < 0:
+        raise KmwsError(d, "kmws_thread_device")
+    return d
 
 
 RESIDENT_EXIT_REASONS = ("lease", "closing", "resize", "idle", "quit")

@@ -11,6 +11,7 @@
 // (links the oracle): tests/test_abi_build.py.
 //
 // usage: txloop_check [seed] [sends]
+//        txloop_check timeout      (linked against the test build: the error path)
 #include <sys/uio.h>
 
 #include <cstdint>
@@ -45,16 +46,85 @@ uint64_t rnd()
     return z ^ (z >> 31);
 }
 
+// a generation whose mask fails is never written.  Needs the test
+// build (kuma_amd/build.py TEST_DEFINES: a resident job whose first key is
+// 0xDEAD5Exx stalls its workgroup xx * 10 ms; timeout 50 ms, drain 150 ms).
+// An 80 ms stall is withdrawn and launched: exact.  A 400 ms stall outlives
+// timeout + drain: the flush returns KMWS_ERR_TIMEOUT, the generation's frames
+// are dropped (not one masked header goes out with a plain payload), their
+// connections report the status, and the loop refuses later sends.
+int timeout_case()
+{
+    std::vector<kmws::TxLoop::Task> tasks;
+    kmws::TxLoop tx([&tasks](kmws::TxLoop::Task t) { tasks.push_back(std::move(t)); }, 0, 64 << 10);
+    if (!tx.valid()) return 3;
+    std::string wrote[2], want[2];
+    kmws::TxLoop::Conn* conn[2];
+    for (int c = 0; c < 2; ++c)
+        conn[c] = tx.open([&wrote, c](const iovec* v, int n) {
+            for (int i = 0; i < n; ++i) wrote[c].append(static_cast<const char*>(v[i].iov_base), v[i].iov_len);
+            return 0;
+        });
+    auto send = [&](int c, uint32_t key, size_t plen, bool expect) {
+        std::vector<uint8_t> payload(plen);
+        for (auto& b : payload) b = (uint8_t)rnd();
+        kmws_frame_hdr h;
+        std::memset(&h, 0, sizeof h);
+        h.fin = 1;
+        h.opcode = KMWS_OP_BINARY;
+        h.mask = 1;
+        std::memcpy(h.maskey, &key, 4);
+        const int r = tx.send(conn[c], h, payload.data(), plen);
+        if (!expect) return r;
+        orc_hdr o;
+        std::memset(&o, 0, sizeof o);
+        o.fin = 1;
+        o.opcode = KMWS_OP_BINARY;
+        o.mask = 1;
+        std::memcpy(o.maskey, &key, 4);
+        o.length = (uint32_t)plen;
+        uint8_t hb[14];
+        const int hl = orc_encode_header(&o, hb);
+        orc_mask(o.maskey, payload.data(), plen, 0);
+        want[c].append(reinterpret_cast<const char*>(hb), (size_t)hl);
+        want[c].append(reinterpret_cast<const char*>(payload.data()), plen);
+        return r;
+    };
+    const uint32_t stall80 = 0xDEAD5E00u | 8, stall400 = 0xDEAD5E00u | 40;
+    int r0 = send(0, 0x11223344u, 3000, true);
+    const int f0 = tx.flush();                  // a normal generation
+    int r1 = send(1, stall80, 5000, true);      // first key of its generation: stalls 80 ms
+    int r2 = send(0, 0x55667788u, 700, true);
+    const int f1 = tx.flush();                  // withdrawn after 50 ms, launched: exact
+    const std::string before0 = wrote[0], before1 = wrote[1];
+    int r3 = send(1, stall400, 4000, false);    // stalls past timeout + drain
+    int r4 = send(0, 0x99AABBCCu, 900, false);
+    const int f2 = tx.flush();
+    const int after = send(0, 0x01010101u, 100, false);
+    const bool dropped_ok = wrote[0] == before0 && wrote[1] == before1 && tx.dropped() == 2 &&
+                            conn[0]->lastResult() == KMWS_ERR_TIMEOUT && conn[1]->lastResult() == KMWS_ERR_TIMEOUT &&
+                            conn[0]->queued() == 0 && conn[1]->queued() == 0;
+    const bool ok = r0 > 0 && r1 > 0 && r2 > 0 && r3 > 0 && r4 > 0 && f0 == 1 && f1 == 2 && f2 == KMWS_ERR_TIMEOUT &&
+                    after == KMWS_ERR_TIMEOUT && tx.broken() == KMWS_ERR_TIMEOUT && !tx.valid() && dropped_ok &&
+                    wrote[0] == want[0] && wrote[1] == want[1];
+    std::printf("{\"case\": \"timeout\", \"flush\": [%d, %d, %d], \"send_after\": %d, \"dropped\": %llu, "
+                "\"conn_results\": [%d, %d], \"bytes\": [%zu, %zu], \"exact\": %s}\n",
+                f0, f1, f2, after, (unsigned long long)tx.dropped(), conn[0]->lastResult(), conn[1]->lastResult(),
+                wrote[0].size(), wrote[1].size(), ok ? "true" : "false");
+    return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
 {
-    g_rng = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
-    const int sends = argc > 2 ? std::atoi(argv[2]) : 3000;
     if (kmws_device_count() < 1) {
         std::printf("{\"error\": \"no gfx950 device\"}\n");
         return 1;
     }
+    if (argc > 1 && std::strcmp(argv[1], "timeout") == 0) return timeout_case();
+    g_rng = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
+    const int sends = argc > 2 ? std::atoi(argv[2]) : 3000;
     std::vector<kmws::TxLoop::Task> tasks;
     constexpr size_t kRing = 64 << 10;  // small: the ring wraps every few iterations
     kmws::TxLoop tx([&tasks](kmws::TxLoop::Task t) { tasks.push_back(std::move(t)); }, 0, kRing);

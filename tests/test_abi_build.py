@@ -231,16 +231,21 @@ def test_rx_flush_bench_every_mode_exact(tmp_path):
     assert rows[0]["resident_jobs"] >= 250 and rows[2]["resident_jobs"] == rows[1]["resident_jobs"]
 
 
-def _build_txloop(tmp_path):
-    """tests/cpp/txloop_check.cpp: kmws::TxLoop against kuma's send path restated in oracle/."""
+def _build_txloop(tmp_path, testhooks=False):
+    """tests/cpp/txloop_check.cpp: kmws::TxLoop against kuma's send path restated in oracle/
+    (testhooks: linked against the test build, kuma_amd/build.py TEST_DEFINES)."""
     lib = kb.build()
+    link = ["-L", os.path.dirname(lib), "-lkmws_gpu"]
+    if testhooks:
+        lib = kb.build_test_variants()[0]
+        link = [os.path.abspath(lib)]
     from oracle import oracle as orc
     orc.build()
     odir = os.path.join(ROOT, "oracle")
-    exe = tmp_path / "txloop_check"
+    exe = tmp_path / ("txloop_check_th" if testhooks else "txloop_check")
     subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
                            os.path.join(ROOT, "tests", "cpp", "txloop_check.cpp"),
-                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle",
+                           *link, "-L", odir, "-lkmws_oracle",
                            "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", str(exe)])
     return exe
 
@@ -262,3 +267,59 @@ def test_txloop_matches_kuma_send_path(tmp_path):
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["exact"] and d["callers_buffers_changed"] == 0 and d["larger_than_ring"] > 0
+
+
+@pytest.mark.gpu
+def test_txloop_mask_failure_drops_the_generation(tmp_path):
+    """ADVICE r05: a TxLoop generation whose mask fails is never written.  Test
+    build: an 80 ms stall is withdrawn and launched (exact); a 400 ms stall
+    outlives timeout + drain, the flush returns KMWS_ERR_TIMEOUT, both of the
+    generation's frames are dropped (no masked header with a plain payload goes
+    out), their connections report -6 and later sends are refused."""
+    import json
+    r = subprocess.run([str(_build_txloop(tmp_path, testhooks=True)), "timeout"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["exact"] and d["flush"] == [1, 2, -6] and d["dropped"] == 2 and d["conn_results"] == [-6, -6]
+
+
+def _build_thread_exit(tmp_path):
+    """tests/cpp/thread_exit_check.cpp: loop threads exiting with frames queued
+    while other threads claim resident slots (VERDICT r05 #1)."""
+    lib = kb.build()
+    from oracle import oracle as orc
+    orc.build()
+    odir = os.path.join(ROOT, "oracle")
+    exe = tmp_path / "thread_exit_check"
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", INC,
+                           os.path.join(ROOT, "tests", "cpp", "thread_exit_check.cpp"),
+                           "-L", os.path.dirname(lib), "-lkmws_gpu", "-L", odir, "-lkmws_oracle", "-lpthread",
+                           "-Wl,-rpath," + os.path.dirname(lib), "-Wl,-rpath," + odir, "-o", str(exe)])
+    return exe
+
+
+def test_thread_exit_program_builds(tmp_path):
+    assert _build_thread_exit(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_thread_exit_with_queued_frames_against_live_claimers(tmp_path):
+    """VERDICT r05 #1.  20 rounds of 8 loop threads that each queue masked frames
+    on a receive and a send loop and exit without flushing (half through
+    RxLoop / TxLoop::forThisThread, half holding raw batches in a thread_local
+    made before their first job, whose flush runs after the thread's exit hook),
+    while 8 other threads keep starting short-lived threads that claim slots and
+    mask 4 KiB buffers.  Every payload received, every frame written and every
+    masked buffer equals the oracle's; no post lands on a slot its thread does
+    not hold; the raw threads' late flushes launched (late posts > 0)."""
+    import json
+    r = subprocess.run([str(_build_thread_exit(tmp_path)), "20", "8", "8"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["exact"] and d["bad_threads"] == 0 and d["mask_bad"] == 0, d
+    assert d["unowned_posts"] == 0 and d["late_posts"] > 0, d
+    q = d["frames_queued_at_exit"]
+    assert q["rx_pending"] > 0 and q["tx_pending"] > 0, d
+    assert d["exited_threads"] == 160 and d["masks"] > 0, d

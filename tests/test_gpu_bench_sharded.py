@@ -31,7 +31,7 @@ def run_bench(*args, timeout=300):
 @pytest.mark.parametrize("job,max_batch", [(65536, 16384), (50001, 20000)])
 def test_bench_two_ranks_shard_the_job(job, max_batch):
     d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--job-frames", str(job), "--max-batch-frames",
-                  str(max_batch), "--steps", "3", "--warmup", "1", "--cpu-seconds", "0")
+                  str(max_batch), "--steps", "3", "--warmup", "1", "--cpu-seconds", "0", "--e2e-gib", "0")
     assert d["n_gpus"] == 2 and d["scaling"] == "strong"
     assert d["verify"]["byte_mismatches"] == 0 and d["verify"]["status_word"] == 0
     ranks = sorted(d["ranks"], key=lambda r: r["rank"])
@@ -51,7 +51,8 @@ def test_bench_two_ranks_shard_the_job(job, max_batch):
 def test_bench_one_gpu_small_batch_plain_rate():
     """N = 1 weak scaling on a small batch, default placement: the timed batch
     is a plain allocation, so the plain rate is the headline's own."""
-    d = run_bench("--frames", "16384", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0")
+    d = run_bench("--frames", "16384", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0", "--cfg5-anchor", "0",
+                  "--e2e-gib", "0")
     assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["verify"]["byte_mismatches"] == 0
     assert d["config"]["placement"]["kind"] == "plain torch.empty"
     assert d["roofline"]["frac_plain"] == d["roofline"]["frac"] > 0  # the timed batch is the plain allocation
@@ -65,6 +66,10 @@ _cfg5 = {}
 def _check_cfg5(d, world):
     assert d["n_gpus"] == world and d["scaling"] == "strong"
     assert d["config"]["total_frames"] == CFG5_FRAMES and d["config"]["frame_len"] == 65536
+    _check_cfg5_ranks(d, world)
+
+
+def _check_cfg5_ranks(d, world):
     assert d["verify"]["byte_mismatches"] == 0 and d["verify"]["status_word"] == 0
     ranks = sorted(d["ranks"], key=lambda r: r["rank"])
     assert [r["rank"] for r in ranks] == list(range(world))
@@ -81,15 +86,21 @@ def _check_cfg5(d, world):
 
 
 @pytest.mark.timeout(600)
-def test_cfg5_full_job_one_gpu():
-    """BASELINE configs[4]'s real job at N = 1 -- 10,485,760 x
-    64 KiB frames as 8 resident sub-batches of 1,310,720 frames (80 GiB), each
-    generated on the device, unmasked by the product kernels and verified byte
-    for byte."""
-    d = run_bench("--gpus", "1", "--job-frames", str(CFG5_FRAMES), "--steps", "2", "--warmup", "1",
-                  "--cpu-seconds", "0", timeout=600)
-    _check_cfg5(d, 1)
-    _cfg5[1] = d["value"]
+def test_cfg5_job_anchor_at_one_gpu():
+    """the N = 1 line (cfg2, here on a small batch) also carries
+    `cfg5_job`, BASELINE configs[4]'s real job -- 10,485,760 x 64 KiB frames as 8
+    resident sub-batches of 1,310,720 frames (80 GiB), each generated on the
+    device, timed as the N > 1 lines time their ranks' sub-batches, verified
+    byte for byte: the same-job anchor of the 1 -> 8 curve."""
+    d = run_bench("--gpus", "1", "--frames", "16384", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0",
+                  "--e2e-gib", "0", timeout=600)
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["config"]["total_frames"] == 16384
+    c = d["cfg5_job"]
+    assert c["total_frames"] == CFG5_FRAMES and c["sub_batches"] == 8 and c["resident_batch_frames"] == CFG5_BATCH
+    assert c["scaling"] == "strong" and c["frame_len"] == 65536
+    _check_cfg5_ranks(c, 1)
+    assert d["verify"]["byte_mismatches"] == 0
+    _cfg5[1] = c["value"]
 
 
 @pytest.mark.timeout(600)
@@ -97,9 +108,11 @@ def test_cfg5_full_job_two_ranks_share_the_gpu():
     """The same job at --gpus 2 (gloo harness, both ranks on the one GPU of the
     box): 4 sub-batches per rank over contiguous shards, every byte verified;
     the two ranks share one GPU's HBM, so the aggregate must stay within 10 %
-    of the N = 1 line (nothing is lost to the partition or the harness)."""
+    of the N = 1 line's cfg5_job value, the same job timed the same way
+    (nothing is lost to the partition or the harness)."""
     d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--job-frames", str(CFG5_FRAMES), "--steps", "2",
-                  "--warmup", "1", "--cpu-seconds", "0", timeout=600)
+                  "--warmup", "1", "--cpu-seconds", "0", "--e2e-gib", "0", timeout=600)
     _check_cfg5(d, 2)
+    assert d["cfg5_job"] is None  # the N > 1 headline is the job itself
     if 1 in _cfg5:
         assert abs(d["value"] / _cfg5[1] - 1) <= 0.10, (d["value"], _cfg5[1])
