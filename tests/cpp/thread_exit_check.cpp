@@ -19,7 +19,7 @@
 // not hold (kmws_resident_guard_counters).  Test infrastructure:
 // tests/test_abi_build.py.
 //
-// usage: thread_exit_check [rounds] [exiters] [maskers]
+// usage: thread_exit_check [rounds] [exiters] [maskers] [both|loop|raw]
 #include <sys/uio.h>
 
 #include <atomic>
@@ -283,6 +283,7 @@ int main(int argc, char** argv)
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 20;
     const int exiters = argc > 2 ? std::atoi(argv[2]) : 8;
     const int maskers = argc > 3 ? std::atoi(argv[3]) : 8;
+    const std::string kinds = argc > 4 ? argv[4] : "both";
     if (kmws_device_count() < 1) {
         std::printf("{\"error\": \"no gfx950 device\"}\n");
         return 1;
@@ -322,7 +323,8 @@ int main(int argc, char** argv)
         std::vector<std::thread> th;
         for (int e = 0; e < exiters; ++e) {
             Out* o = &outs[(size_t)e];
-            if (e % 2 == 0) th.emplace_back([o] { loop_exiter(o); });
+            const bool loop = kinds == "loop" || (kinds == "both" && e % 2 == 0);
+            if (loop) th.emplace_back([o] { loop_exiter(o); });
             else th.emplace_back([o] { raw_exiter(o); });
         }
         for (auto& t : th) t.join();
@@ -334,7 +336,7 @@ int main(int argc, char** argv)
                 if (first_why.empty()) first_why = "round " + std::to_string(r) + " thread " + std::to_string(e) + ": " + why;
             }
             ++exited;
-            (e % 2 == 0 ? loop_ex : raw_ex)++;
+            ((kinds == "loop" || (kinds == "both" && e % 2 == 0)) ? loop_ex : raw_ex)++;
             rx_pending += o.rx_pending_at_exit;
             rx_inflight += o.rx_inflight_at_exit;
             tx_pending += o.tx_pending_at_exit;
