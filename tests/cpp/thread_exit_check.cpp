@@ -213,11 +213,18 @@ RawHolder& raw_holder()
 
 void raw_exiter(Out* o)
 {
+    // The batches first: the thread's first HIP calls set up the HIP runtime's
+    // own per-thread state, which C++ then destroys AFTER the holder below (a
+    // thread_local made before a thread's first HIP call must not call HIP from
+    // its destructor: the runtime's per-thread objects are gone by then).
+    kmws_rx_batch* rb = kmws_rx_batch_create(KMWS_DEVICE_AUTO);
+    kmws_decoder* dec = kmws_decoder_create(KMWS_MODE_SERVER, KMWS_DEVICE_AUTO);
+    kmws_tx_batch* tb = kmws_tx_batch_create(KMWS_DEVICE_AUTO);
     RawHolder& r = raw_holder();  // before any resident job: no exit hook yet
     r.o = o;
-    r.rb = kmws_rx_batch_create(KMWS_DEVICE_AUTO);
-    r.dec = kmws_decoder_create(KMWS_MODE_SERVER, KMWS_DEVICE_AUTO);
-    r.tb = kmws_tx_batch_create(KMWS_DEVICE_AUTO);
+    r.rb = rb;
+    r.dec = dec;
+    r.tb = tb;
     if (!r.rb || !r.dec || !r.tb) {
         o->err = 10;
         return;
