@@ -188,6 +188,19 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Write-through (sc0 sc1: system scope) stores of the job's payload bytes.
+// Complete -- written through to host memory -- once the storing wave's
+// vmcnt drains, so the done word needs no release: a system-scope release is
+// a buffer_wbl2 of the whole XCD L2, which at a million small jobs a second
+// stalled a device batch running beside the grid (tools/grid_interference).
+__device__ __forceinline__ void st_sys16(uint64_t a, u32x4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sys1(uint64_t a, uint32_t v)
+{
+    asm volatile("global_store_byte %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"(v) : "memory");
+}
 // ResCtl lives in uncached device memory (ResidentWorker::init), so a plain
 // load of a word other XCDs update is never served stale from this XCD's L2
 // (a read-modify-write would be coherent too, but 64 workgroups doing one on
@@ -390,13 +403,13 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 const uint64_t end = x.addr + x.len;
                 const uint32_t r = rot_key(x.key, x.addr);
                 if (a >= x.addr && a + 16 <= end) {
-                    *reinterpret_cast<u32x4*>(a) = v[i] ^ r;
+                    st_sys16(a, v[i] ^ r);
                 } else {  // a hull's first or last word: this payload's bytes only
                     const uint64_t lo = a > x.addr ? a : x.addr, hi = a + 16 < end ? a + 16 : end;
                     for (uint64_t q = lo; q < hi; ++q) {
                         const uint32_t b = (uint32_t)(q - a);
                         const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
-                        *reinterpret_cast<uint8_t*>(q) = (uint8_t)((dw ^ r) >> (8 * (b & 3u)));
+                        st_sys1(q, (dw ^ r) >> (8 * (b & 3u)));
                     }
                 }
             }
@@ -408,7 +421,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         // (tools/zc_probe.hip, profiles/r05n_zc_probe.jsonl).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t == 0) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (t < 64) {
             last = cmd & kJobMask;
             t_act = wall_clock64();  // the slot was busy until now (a long job is not idle time)

@@ -14,7 +14,12 @@
 // `rocprofv3 --kernel-trace --stats` to see the same launches from the trace
 // (tools/gpu_interference.sh).
 //
-// usage: grid_interference [frames] [steps] [phases] [threads]
+// Attribution modes (5th argument): resident (the above), launch (the same
+// masks with the grid switched off in every masking thread: a launch per
+// call), one (thread 0 masks; the others claim a slot with one mask per phase
+// and then idle, so the grid polls 16 claimed slots while one works).
+//
+// usage: grid_interference [frames] [steps] [phases] [threads] [resident|launch|one]
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -36,6 +41,7 @@ int main(int argc, char** argv)
     const int steps = argc > 2 ? std::atoi(argv[2]) : 20;
     const int phases = argc > 3 ? std::atoi(argv[3]) : 6;
     const int threads = argc > 4 ? std::atoi(argv[4]) : 16;
+    const std::string how = argc > 5 ? argv[5] : "resident";
     if (kmws_device_count() < 1) {
         std::printf("{\"error\": \"no gfx950 device\"}\n");
         return 1;
@@ -72,10 +78,14 @@ int main(int argc, char** argv)
         th.emplace_back([&, t] {
             std::vector<uint8_t> a(4096, (uint8_t)t), b;
             uint8_t key[4] = {(uint8_t)(t + 1), 0x5A, 0xC3, 0x96};
+            if (how == "launch") kmws_resident_enable(0, 0);
+            int last_mode = 0;
             for (;;) {
                 const int m = mode.load(std::memory_order_acquire);
                 if (m < 0) break;
-                if (m == 0) {
+                const bool fresh = m != last_mode;
+                last_mode = m;
+                if (m == 0 || (how == "one" && t != 0 && !fresh)) {
                     std::this_thread::sleep_for(std::chrono::microseconds(200));
                     continue;
                 }
@@ -142,10 +152,10 @@ int main(int argc, char** argv)
     uint64_t jobs = 0, launches = 0;
     kmws_resident_info(0, &jobs, &launches, nullptr);
     const double q = sum_q / (nq ? nq : 1), b = sum_b / (nb ? nb : 1);
-    std::printf("{\"frames\": %u, \"frame_len\": %llu, \"steps_per_phase\": %d, \"threads\": %d, \"phases\": [%s], "
+    std::printf("{\"mode\": \"%s\", \"frames\": %u, \"frame_len\": %llu, \"steps_per_phase\": %d, \"threads\": %d, \"phases\": [%s], "
                 "\"quiet_mean_ms\": %.4f, \"busy_mean_ms\": %.4f, \"busy_over_quiet\": %.4f, \"resident_jobs\": %llu, "
                 "\"grid_launches\": %llu, \"mask_bad\": %ld, \"byte_mismatches\": %llu}\n",
-                n, (unsigned long long)L, steps, threads, rows.c_str(), q, b, b / q, (unsigned long long)jobs,
+                how.c_str(), n, (unsigned long long)L, steps, threads, rows.c_str(), q, b, b / q, (unsigned long long)jobs,
                 (unsigned long long)launches, bad.load(), mm);
     return mm == 0 && bad.load() == 0 ? 0 : 1;
 }
