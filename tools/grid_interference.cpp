@@ -19,7 +19,10 @@
 // call), one (thread 0 masks; the others claim a slot with one mask per phase
 // and then idle, so the grid polls 16 claimed slots while one works).
 //
-// usage: grid_interference [frames] [steps] [phases] [threads] [resident|launch|one]
+// one_50us / one_1ms: as one, thread 0 sleeping that long between its masks.
+// claim: every thread masks once per busy phase (claims its slot) and idles.
+//
+// usage: grid_interference [frames] [steps] [phases] [threads] [resident|launch|one|one_50us|one_1ms|claim]
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -85,7 +88,8 @@ int main(int argc, char** argv)
                 if (m < 0) break;
                 const bool fresh = m != last_mode;
                 last_mode = m;
-                if (m == 0 || (how == "one" && t != 0 && !fresh)) {
+                const bool one = how.rfind("one", 0) == 0;
+                if (m == 0 || (one && t != 0 && !fresh) || (how == "claim" && !fresh)) {
                     std::this_thread::sleep_for(std::chrono::microseconds(200));
                     continue;
                 }
@@ -96,6 +100,8 @@ int main(int argc, char** argv)
                 for (size_t i = 0; i < b.size(); ++i) b[i] ^= key[i & 3];
                 if (a != b) ++bad;
                 masks.fetch_add(1, std::memory_order_relaxed);
+                if (t == 0 && how == "one_50us") std::this_thread::sleep_for(std::chrono::microseconds(50));
+                if (t == 0 && how == "one_1ms") std::this_thread::sleep_for(std::chrono::milliseconds(1));
             }
         });
 

@@ -40,20 +40,47 @@
 //  8  one wave: between polls it reads and rewrites a 4 KiB block of pinned
 //     host memory (write-through), then sleeps ~4 us: a trickle of PCIe
 //     traffic, like a few resident jobs a second
+// Configurations "relaunch_*": a host thread relaunches the spinner every
+// millisecond (releases it, waits for it, launches it again), as the resident
+// grid's lease does.
+// Configurations "*_hostread" / "*_hostwrite": beside the spinner (5: 64
+// workgroups, wave 0 polling its own host word), a host thread spins reading a
+// pinned word on a line of its own / writes the second word of each polled
+// line in turn (the polled words keep their value), as a loop thread posting
+// jobs and waiting for them does.
+// Configurations "*_stages": first 16 host threads each run one kmws mask
+// with the resident grid off for them (each borrows a pinned stage with its
+// own stream, as loop threads do), so the process holds as many streams as a
+// loop-thread process.
 // Configuration "sdma": no spinner; a host thread keeps 4 MiB pinned H2D and
 // D2H copies running on another stream during the timed applies.
 // Device flags are released by a copy of the host flag.
-__global__ void spin_kernel(uint64_t* hflag, uint64_t* dflag_uc, uint64_t* dflag, int how)
+//  9  as 8 on ordinary (non-coherent, hipHostMallocDefault) pinned memory
+//     with plain 16-byte loads and stores, as the staging of the resident jobs
+// 10  as 9 with write-through (sc0 sc1) stores, as the resident grid's
+__global__ void spin_kernel(uint64_t* hflag, uint64_t* dflag_uc, uint64_t* dflag, int how, uint8_t* nc)
 {
-    uint64_t* f = how == 2 ? dflag_uc : how == 3 ? dflag : how >= 5 ? hflag + 32 * (blockIdx.x % 64) : hflag;
+    uint64_t* f = how == 2 ? dflag_uc : how == 3 ? dflag : (how >= 5 && how <= 7) ? hflag + 32 * (blockIdx.x % 64) : hflag;
     uint64_t clk = 0;
-    const bool poller = how < 4 || threadIdx.x < 64;
+    const bool poller = how < 4 || how >= 8 || threadIdx.x < 64;
     if (poller) {
         for (;;) {
             const uint64_t v = how == 2 || how == 3 ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                                     : __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (__builtin_amdgcn_readfirstlane((int)v)) break;
             if (how == 6) clk += __builtin_amdgcn_s_memrealtime();
+            if ((how == 9 || how == 10) && threadIdx.x < 64) {
+                typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+                for (int i = 0; i < 4; ++i) {
+                    v4* q = reinterpret_cast<v4*>(nc) + threadIdx.x + 64 * i;
+                    v4 x = *q;
+                    x.x += 1;
+                    if (how == 9) *q = x;
+                    else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(q), "v"(x) : "memory");
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_sleep(127);
+            }
             if (how == 8 && threadIdx.x < 64) {
                 uint64_t* blk = hflag + 4096;  // 4 KiB at +32 KiB of the flag area
                 for (int i = 0; i < 8; ++i) {
@@ -67,7 +94,7 @@ __global__ void spin_kernel(uint64_t* hflag, uint64_t* dflag_uc, uint64_t* dflag
             else __builtin_amdgcn_s_sleep(2);
         }
     }
-    if (how >= 4) __syncthreads();
+    if (how >= 4 && how <= 7) __syncthreads();
     if (clk == 0x123456789ull) hflag[1] = clk;  // keeps the clock reads
 }
 
@@ -92,6 +119,9 @@ int main(int argc, char** argv)
     uint64_t* flag = nullptr;
     (void)hipHostMalloc(reinterpret_cast<void**>(&flag), 64 * 1024, hipHostMallocCoherent | hipHostMallocMapped);
     uint64_t *duc = nullptr, *dl2 = nullptr;
+    uint8_t *nch = nullptr, *ncbuf = nullptr;
+    (void)hipHostMalloc(reinterpret_cast<void**>(&nch), 1 << 16, hipHostMallocDefault);
+    (void)hipHostGetDevicePointer(reinterpret_cast<void**>(&ncbuf), nch, 0);
     (void)hipExtMallocWithFlags(reinterpret_cast<void**>(&duc), 256, hipDeviceMallocUncached);
     (void)hipMalloc(reinterpret_cast<void**>(&dl2), 256);
     uint64_t* dflag = nullptr;
@@ -107,7 +137,8 @@ int main(int argc, char** argv)
         const char* name;
         int wgs, lanes, prio, how;
     };
-    const Cfg cfgs[] = {{"none", 0, 0, 0, 0}, {"pcie_trickle_1x64", 1, 64, 1, 8}, {"sdma", 0, 0, 0, 0},
+    const Cfg cfgs[] = {{"none", 0, 0, 0, 0}, {"own16", 16, 1024, 1, 5}, {"none_stages", 0, 0, 0, 0},
+                        {"own16_after_stages", 16, 1024, 1, 5}, {"own16_np_after_stages", 16, 1024, 0, 5},
                         {"none", 0, 0, 0, 0}};
     std::vector<uint8_t> dummy;
     uint8_t *hbuf = nullptr, *dbuf = nullptr;
@@ -124,16 +155,61 @@ int main(int argc, char** argv)
         (void)hipMemcpyAsync(dl2, &one, 8, hipMemcpyHostToDevice, rs);
         (void)hipStreamSynchronize(rs);
     };
+    bool staged = false;
     for (const Cfg& c : cfgs) {
+        const std::string nm = c.name;
+        if (nm.find("stages") != std::string::npos && !staged) {
+            std::vector<std::thread> ts;
+            for (int t = 0; t < 16; ++t)
+                ts.emplace_back([] {
+                    kmws_resident_enable(0, 0);
+                    std::vector<uint8_t> a(4096, 1);
+                    uint8_t key[4] = {1, 2, 3, 4};
+                    uint8_t* seg = a.data();
+                    size_t len = a.size();
+                    (void)kmws_mask_host_chain(key, &seg, &len, 1, 0);
+                });
+            for (auto& t : ts) t.join();
+            staged = true;
+        }
         std::memset(flag, 0, 64 * 1024);
         (void)hipMemset(duc, 0, 256);
         (void)hipMemset(dl2, 0, 256);
         (void)hipDeviceSynchronize();
-        if (c.wgs) {
-            hipLaunchKernelGGL(spin_kernel, dim3(c.wgs), dim3(c.lanes), 0, c.prio ? hp : np, dflag, duc, dl2, c.how);
+        const bool relaunch = std::string(c.name).rfind("relaunch", 0) == 0;
+        std::atomic<bool> relaunching{relaunch};
+        std::thread relauncher;
+        if (c.wgs && !relaunch) {
+            hipLaunchKernelGGL(spin_kernel, dim3(c.wgs), dim3(c.lanes), 0, c.prio ? hp : np, dflag, duc, dl2, c.how, ncbuf);
             std::this_thread::sleep_for(std::chrono::milliseconds(5));
         }
+        if (relaunch)
+            relauncher = std::thread([&] {
+                hipStream_t q = c.prio ? hp : np;
+                while (relaunching.load()) {
+                    for (int i = 0; i < 64; ++i) __atomic_store_n(flag + 32 * i, 0ull, __ATOMIC_RELEASE);
+                    hipLaunchKernelGGL(spin_kernel, dim3(c.wgs), dim3(c.lanes), 0, q, dflag, duc, dl2, c.how, ncbuf);
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                    for (int i = 0; i < 64; ++i) __atomic_store_n(flag + 32 * i, 1ull, __ATOMIC_RELEASE);
+                    (void)hipStreamSynchronize(q);
+                }
+            });
         std::atomic<bool> copying{std::string(c.name) == "sdma"};
+        std::atomic<bool> hosting{nm.find("_host") != std::string::npos};
+        std::thread hoster([&] {
+            uint64_t sink = 0, i = 0;
+            const bool wr = nm.find("hostwrite") != std::string::npos;
+            while (hosting.load(std::memory_order_relaxed)) {
+                if (wr) {
+                    __atomic_store_n(flag + 32 * (i % 64) + 1, i, __ATOMIC_RELEASE);
+                    for (int k = 0; k < 200; ++k) __builtin_ia32_pause();
+                } else {
+                    sink += __atomic_load_n(flag + 32 * 64 + 8, __ATOMIC_ACQUIRE);
+                }
+                ++i;
+            }
+            if (sink == 42) std::printf("#");
+        });
         std::thread copier([&] {
             while (copying.load()) {
                 (void)hipMemcpyAsync(dbuf, hbuf, 4u << 20, hipMemcpyHostToDevice, cs);
@@ -145,7 +221,31 @@ int main(int argc, char** argv)
         double tot = 0;
         const int steps = 20;
         bool queued_behind = false;
-        for (int i = 0; i < steps; ++i) {
+        const bool batched = nm.find("_q20") != std::string::npos;
+        std::vector<hipEvent_t> evs(2 * steps);
+        if (batched) {
+            for (auto& e : evs) (void)hipEventCreate(&e);
+            for (int i = 0; i < steps; ++i) {
+                (void)hipEventRecord(evs[2 * i], s);
+                (void)kmws_unmask_apply(base, span, descs, n, ws, wsb, s);
+                (void)hipEventRecord(evs[2 * i + 1], s);
+            }
+            const auto t0 = std::chrono::steady_clock::now();
+            while (hipEventQuery(evs[2 * steps - 1]) == hipErrorNotReady) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10) && !queued_behind) {
+                    release();
+                    queued_behind = true;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(100));
+            }
+            for (int i = 0; i < steps; ++i) {
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, evs[2 * i], evs[2 * i + 1]);
+                tot += ms;
+            }
+            for (auto& e : evs) (void)hipEventDestroy(e);
+        }
+        for (int i = 0; i < (batched ? 0 : steps); ++i) {
             (void)hipEventRecord(e0, s);
             (void)kmws_unmask_apply(base, span, descs, n, ws, wsb, s);
             (void)hipEventRecord(e1, s);
@@ -164,6 +264,10 @@ int main(int argc, char** argv)
             (void)hipEventElapsedTime(&ms, e0, e1);
             tot += ms;
         }
+        relaunching.store(false);
+        if (relauncher.joinable()) relauncher.join();
+        hosting.store(false);
+        hoster.join();
         release();
         copying.store(false);
         copier.join();
