@@ -811,7 +811,16 @@ private:
             (void)hipGetLastError();
             greatest = least = 0;
         }
-        if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest) != hipSuccess) {
+        // The grid runs on the SECOND greatest-priority stream this worker makes:
+        // on the first one, a device batch beside the grid ran 1.33-1.40x slower
+        // (cfg2, 0.82 -> 0.59 of HBM peak) whatever the grid did -- its jobs, its
+        // polls, its block size, its lease (every such variant measured, and a
+        // probe kernel of the grid's shape on a stream of its own slowed nothing);
+        // with a greatest-priority stream made before it the same grid cost
+        // 1.02x under 16 threads' 4 KiB masks (tools/grid_interference.cpp,
+        // tools/priority_probe.hip, profiles/r06ag_*).  The spare stays unused.
+        if (hipStreamCreateWithPriority(&spare_stream_, hipStreamNonBlocking, greatest) != hipSuccess ||
+            hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest) != hipSuccess) {
             (void)hipGetLastError();
             return KMWS_ERR_FAILED;
         }
@@ -879,6 +888,7 @@ private:
     ResMailbox* dmb_ = nullptr;
     ResCtl* dctl_ = nullptr;
     hipStream_t stream_ = nullptr;
+    hipStream_t spare_stream_ = nullptr;  // made first, never used (see init)
     uint64_t idle_ticks_ = 0, lease_ticks_ = 0;
     uint64_t inc_ = 0;  // latest incarnation launched
     uint32_t nslots_ = 0;     // slots the latest incarnation serves

@@ -63,6 +63,21 @@ int main(int argc, char** argv)
     }
     hipStream_t s;
     (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (std::getenv("GI_PRESTREAMS")) {  // harness variant: the streams tools/priority_probe.hip creates first
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        hipStream_t hp, np, cs, rs;
+        (void)hipStreamCreateWithPriority(&hp, hipStreamNonBlocking, greatest);
+        (void)hipStreamCreateWithPriority(&np, hipStreamNonBlocking, least);
+        (void)hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+        (void)hipStreamCreateWithPriority(&rs, hipStreamNonBlocking, greatest);
+    }
+    if (std::getenv("GI_HPONE")) {  // harness variant: one high-priority stream only
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        hipStream_t hp;
+        (void)hipStreamCreateWithPriority(&hp, hipStreamNonBlocking, greatest);
+    }
     const uint64_t seed = 0x6B756D61;
     if (kmws_fill_synthetic(base, span, seed, s) != KMWS_OK ||
         kmws_fill_uniform_descs(descs, n, L, (uint32_t)L, seed ^ 0x5EED, s) != KMWS_OK ||
@@ -118,10 +133,18 @@ int main(int argc, char** argv)
         else std::this_thread::sleep_for(std::chrono::milliseconds(5));        // the grid idles out (200 us)
         const long m0 = masks.load();
         const auto t0 = std::chrono::steady_clock::now();
+        const bool one_by_one = std::getenv("GI_ONE") != nullptr;  // harness variant: wait for each apply
         for (int i = 0; i < steps; ++i) {
             (void)hipEventRecord(ev[2 * (size_t)i], s);
             (void)kmws_unmask_apply(base, span, descs, n, ws, wsb, s);
             (void)hipEventRecord(ev[2 * (size_t)i + 1], s);
+            if (one_by_one)
+                while (hipEventQuery(ev[2 * (size_t)i + 1]) == hipErrorNotReady)
+                    std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        if (std::getenv("GI_POLL")) {  // harness variant: poll the last event instead of a blocking synchronize
+            while (hipEventQuery(ev[2 * (size_t)steps - 1]) == hipErrorNotReady)
+                std::this_thread::sleep_for(std::chrono::microseconds(100));
         }
         (void)hipStreamSynchronize(s);
         const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -52,6 +52,10 @@
 // with the resident grid off for them (each borrows a pinned stage with its
 // own stream, as loop threads do), so the process holds as many streams as a
 // loop-thread process.
+// Configuration "grid_claim16": 16 host threads each run one kmws mask on the
+// resident grid (claiming their slots) and stay alive until the
+// configuration ends; run with a keep-alive build of the library
+// (tools/patches/meas_keepalive.patch) the grid then stays on the GPU.
 // Configuration "sdma": no spinner; a host thread keeps 4 MiB pinned H2D and
 // D2H copies running on another stream during the timed applies.
 // Device flags are released by a copy of the host flag.
@@ -137,9 +141,8 @@ int main(int argc, char** argv)
         const char* name;
         int wgs, lanes, prio, how;
     };
-    const Cfg cfgs[] = {{"none", 0, 0, 0, 0}, {"own16", 16, 1024, 1, 5}, {"none_stages", 0, 0, 0, 0},
-                        {"own16_after_stages", 16, 1024, 1, 5}, {"own16_np_after_stages", 16, 1024, 0, 5},
-                        {"none", 0, 0, 0, 0}};
+    const Cfg cfgs[] = {{"none", 0, 0, 0, 0}, {"own16", 16, 1024, 1, 5}, {"grid_claim16", 0, 0, 0, 0},
+                        {"none_after_grid", 0, 0, 0, 0}};
     std::vector<uint8_t> dummy;
     uint8_t *hbuf = nullptr, *dbuf = nullptr;
     (void)hipHostMalloc(reinterpret_cast<void**>(&hbuf), 8u << 20, hipHostMallocDefault);
@@ -195,6 +198,20 @@ int main(int argc, char** argv)
                 }
             });
         std::atomic<bool> copying{std::string(c.name) == "sdma"};
+        std::atomic<bool> claiming{nm == "grid_claim16"};
+        std::vector<std::thread> claimers;
+        if (claiming.load()) {
+            for (int t = 0; t < 16; ++t)
+                claimers.emplace_back([&claiming, t] {
+                    std::vector<uint8_t> a(4096, (uint8_t)t);
+                    uint8_t key[4] = {(uint8_t)t, 2, 3, 4};
+                    uint8_t* seg = a.data();
+                    size_t len = a.size();
+                    (void)kmws_mask_host_chain(key, &seg, &len, 1, 0);
+                    while (claiming.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                });
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
         std::atomic<bool> hosting{nm.find("_host") != std::string::npos};
         std::thread hoster([&] {
             uint64_t sink = 0, i = 0;
@@ -268,6 +285,8 @@ int main(int argc, char** argv)
         if (relauncher.joinable()) relauncher.join();
         hosting.store(false);
         hoster.join();
+        claiming.store(false);
+        for (auto& t : claimers) t.join();
         release();
         copying.store(false);
         copier.join();
