@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--cfg5-anchor", type=int, default=1,
                    help="N = 1 cfg2 run: also time BASELINE configs[4]'s whole job (cfg5_job key), the same-job "
                         "anchor of the N > 1 curve (0 = skip)")
-    p.add_argument("--e2e-gib", type=float, default=2.0,
+    p.add_argument("--e2e-gib", type=float, default=4.0,
                    help="host-resident end-to-end shard per rank in GiB: the e2e_host key of a cfg2 run "
                         "(0 = skip), or the workload of --config e2e")
     p.add_argument("--steps", type=int, default=20)
@@ -874,7 +874,7 @@ def main():
     if a.e2e_gib > 0:
         try:
             e2e = run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev, gib=a.e2e_gib,
-                          steps=min(a.steps, 5), warmup=1)
+                          steps=min(a.steps, 5), warmup=2)
         except Exception as ex:  # recorded, never masking the headline
             e2e = {"error": repr(ex)}
 
