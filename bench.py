@@ -852,6 +852,15 @@ def main():
         return
 
     L = a.frame_len
+    # The host-resident leg first, in a fresh process (after the 64-80 GiB device
+    # jobs the same 4 GiB shard ran at 36 instead of 44.7 GiB/s: r06ai vs r06aj).
+    e2e = None
+    if a.e2e_gib > 0:
+        try:
+            e2e = run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev, gib=a.e2e_gib,
+                          steps=min(a.steps, 5), warmup=2)
+        except Exception as ex:  # recorded, never masking the headline
+            e2e = {"error": repr(ex)}
     r = run_job(a, kmws, torch, dist, dev, coll_dev, rank, world, job_frames, shared_gpu)
     # At N = 1 the headline is cfg2 (weak); the N > 1 lines run BASELINE
     # configs[4]'s fixed job (strong).  So that the 1 -> 8 curve has a same-job
@@ -870,13 +879,6 @@ def main():
                         "per sub-batch, generated on device untimed, barrier + synchronize around the timed "
                         "steps, step time = sum over sub-batches; the N > 1 lines' value over this value is "
                         "their speed-up"}
-    e2e = None
-    if a.e2e_gib > 0:
-        try:
-            e2e = run_e2e(a, kmws, torch, dist, dev, coll_dev, rank, world, ndev, gib=a.e2e_gib,
-                          steps=min(a.steps, 5), warmup=2)
-        except Exception as ex:  # recorded, never masking the headline
-            e2e = {"error": repr(ex)}
 
     ms_per_step = r["ms_per_step"]
     value = r["value"]  # = shard.aggregate_rate over ranks (elapsed = max)
