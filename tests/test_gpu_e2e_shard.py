@@ -104,3 +104,14 @@ def test_device_policy_on_the_box():
     buf = bytearray(data)
     kmws.handle_data_mask(key, [buf], device=kmws.DEVICE_AUTO)
     assert bytes(buf) == orc.mask_bytes(key, data)
+
+
+def test_two_rank_bench_line_carries_e2e_host():
+    """The N > 1 line (here two gloo ranks on the one GPU, a small strong-scaling
+    job) carries the host-resident leg too: both ranks' shards verified."""
+    d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--job-frames", "65536", "--max-batch-frames", "16384",
+                  "--steps", "2", "--warmup", "1", "--cpu-seconds", "0", "--e2e-gib", "0.25")
+    e = d["e2e_host"]
+    assert "error" not in e, e
+    assert e["n_gpus"] == 2 and len(e["ranks"]) == 2 and e["verify"]["ok"]
+    assert d["verify"]["byte_mismatches"] == 0 and d["cfg5_job"] is None
