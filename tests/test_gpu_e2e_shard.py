@@ -7,6 +7,7 @@ its own shard of masked 64 KiB frames into pinned host memory
 (kmws_host_alloc), unmasks it in place end to end through its own
 kmws_pipeline (pinned H2D -> unmask kernel -> D2H), and verifies every byte on
 the device.  No data-path collective."""
+import ctypes
 import json
 import os
 import subprocess
@@ -83,8 +84,8 @@ def test_device_policy_on_the_box():
         res["dev"] = L.kmws_thread_device()
         res["pin_bad"] = L.kmws_set_thread_device(ndev)
         res["attach"] = L.kmws_thread_attach(kmws.DEVICE_AUTO)
-        node = __import__("ctypes").c_int(-2)
-        res["node"] = (L.kmws_device_numa_node(0, __import__("ctypes").byref(node)), node.value)
+        node = ctypes.c_int(-2)
+        res["node"] = (L.kmws_device_numa_node(0, ctypes.byref(node)), node.value)
 
     t = threading.Thread(target=pinned)
     t.start()
