@@ -49,6 +49,13 @@ namespace kmws {
 
 constexpr int kResBlock = 1024;  // 16 waves: 4 words each = 64 KiB of loads in flight
 constexpr int kResWords = 4;
+// Jobs of up to this many 16-byte words store write-through (sc0 sc1) and end
+// without a release; larger ones store into the L2 and end with one
+// system-scope release (a buffer_wbl2 of the XCD's L2).  A release per job at
+// a million small jobs a second slowed a device batch beside the grid
+// (tools/grid_interference.cpp); write-through stores of 64 KiB generations
+// halved 8 loopback connections' decode (18.6 -> 8.6-10.9 GiB/s, r06an-ap).
+constexpr int kResWriteThroughWords = 1024;
 // Slots per device: one per loop thread that uses the synchronous entries
 // (kuma's test client runs 10 loop threads, its server 5).  Unclaimed slots'
 // workgroups poll one word every few microseconds; a claimed slot's workgroup
@@ -188,18 +195,49 @@ __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// Write-through (sc0 sc1: system scope) stores of the job's payload bytes.
-// Complete -- written through to host memory -- once the storing wave's
-// vmcnt drains, so the done word needs no release: a system-scope release is
-// a buffer_wbl2 of the whole XCD L2, which at a million small jobs a second
-// stalled a device batch running beside the grid (tools/grid_interference).
-__device__ __forceinline__ void st_sys16(uint64_t a, u32x4 v)
+// Write-through (sc0 sc1: system scope) stores of a small job's payload
+// bytes (kResWriteThroughWords).  Complete -- written through to host memory
+// -- once the storing wave's vmcnt drains, so the done word needs no release:
+// a system-scope release is a buffer_wbl2 of the whole XCD L2, which at a
+// million small jobs a second stalled a device batch running beside the grid
+// (tools/grid_interference.cpp).  A lane's four words go in ONE asm
+// statement: the compiler waits for every access in flight before an inline
+// asm, so four statements made each store wait for the one before.  Flat
+// stores: a lane with nothing to store aims its words at its own 16 bytes of
+// LDS (no memory traffic).  8-byte stores the compiler could count instead
+// wrote half of every 16 bytes per instruction and ran 10x slower (r06ao).
+__device__ __forceinline__ void st_sys16x4(uint64_t a0, u32x4 v0, uint64_t a1, u32x4 v1, uint64_t a2, u32x4 v2,
+                                           uint64_t a3, u32x4 v3)
 {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"(v) : "memory");
+    asm volatile(
+        "flat_store_dwordx4 %0, %1 sc0 sc1\n\t"
+        "flat_store_dwordx4 %2, %3 sc0 sc1\n\t"
+        "flat_store_dwordx4 %4, %5 sc0 sc1\n\t"
+        "flat_store_dwordx4 %6, %7 sc0 sc1\n\t"
+        "s_nop 1" ::"v"(a0),
+        "v"(v0), "v"(a1), "v"(v1), "v"(a2), "v"(v2), "v"(a3), "v"(v3)
+        : "memory");
 }
+// The same four words into the L2 (write-back): a large job's stores, made
+// visible by one release at its end (see kResWriteThroughWords).
+__device__ __forceinline__ void st_l2_16x4(uint64_t a0, u32x4 v0, uint64_t a1, u32x4 v1, uint64_t a2, u32x4 v2,
+                                           uint64_t a3, u32x4 v3)
+{
+    asm volatile(
+        "flat_store_dwordx4 %0, %1\n\t"
+        "flat_store_dwordx4 %2, %3\n\t"
+        "flat_store_dwordx4 %4, %5\n\t"
+        "flat_store_dwordx4 %6, %7\n\t"
+        "s_nop 1" ::"v"(a0),
+        "v"(v0), "v"(a1), "v"(v1), "v"(a2), "v"(v2), "v"(a3), "v"(v3)
+        : "memory");
+}
+// A small job's hull edge bytes, written through: stores the compiler counts
+// (no wait between them); a large job's edge bytes are plain stores.
 __device__ __forceinline__ void st_sys1(uint64_t a, uint32_t v)
 {
-    asm volatile("global_store_byte %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"(v) : "memory");
+    __hip_atomic_store(reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(a), (uint8_t)v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // ResCtl lives in uncached device memory (ResidentWorker::init), so a plain
 // load of a word other XCDs update is never served stale from this XCD's L2
@@ -232,10 +270,12 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     __shared__ uint32_t s_pre[kResMaxDescs + 1];  // word prefix over the payload hulls
     __shared__ uint64_t s_cmd;
     __shared__ uint32_t s_have;  // descriptors taken from the poll
+    __shared__ u32x4 s_sink[kResBlock];  // per lane: the words of a lane with none to load or store
     const int t = threadIdx.x;
     const uint32_t part = blockIdx.x / nslots;
     ResSlot* sl = &mb->slot[(blockIdx.x % nslots + nslots - part % nslots) % nslots];
     const uint64_t born = wall_clock64();
+    const uint64_t my_sink = reinterpret_cast<uint64_t>(static_cast<void*>(&s_sink[t]));  // a flat (LDS) address
     // lane l <= kPollDescs of wave 0 of part 0 polls bytes [16 l, 16 l + 16)
     // of the slot: the job word (lane 0) and descriptor slot l - 1; other
     // parts, and part 0 while the slot is unclaimed, load the word only (one
@@ -373,55 +413,79 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         }
         __syncthreads();
         const uint32_t total = s_pre[n];
+        const bool wt = total <= (uint32_t)kResWriteThroughWords;  // the same in every part
         // this part's words: an even share, in job order
         const uint32_t wb = (uint32_t)((uint64_t)total * part / parts), we = (uint32_t)((uint64_t)total * (part + 1) / parts);
         for (uint32_t w0 = wb; w0 < we; w0 += kResBlock * kResWords) {
+            if (w0 + (uint32_t)(t & ~63) >= we) break;  // nothing left for this wave (uniform)
             u32x4 v[kResWords];
             uint32_t di[kResWords];
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
+                // a lane past the part's end loads its LDS sink (clamped to the
+                // part's last word, many waves reading one host word stalled
+                // the grid: 4 KiB jobs ran at 48 us, r06ao)
                 const uint32_t w = w0 + t + kResBlock * i;
-                di[i] = 0;
-                v[i] = u32x4{0, 0, 0, 0};
-                if (w < we) {
-                    uint32_t lo = 0, hi = n;  // last payload whose first word is <= w
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_pre[mid] <= w) lo = mid; else hi = mid;
-                    }
-                    di[i] = lo;
-                    const ResDesc x = s_d[lo];
-                    v[i] = *reinterpret_cast<const u32x4*>(((x.addr >> 4) + (w - s_pre[lo])) << 4);
+                uint32_t lo = 0, hi = n;  // last payload whose first word is <= w
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= w) lo = mid; else hi = mid;
                 }
+                di[i] = lo;
+                const ResDesc x = s_d[lo];
+                const uint64_t a = w < we ? ((x.addr >> 4) + (w - s_pre[lo])) << 4 : my_sink;
+                v[i] = *reinterpret_cast<const u32x4*>(a);  // flat: host memory, or the lane's LDS sink
             }
+            // whole words first, in one asm statement; a hull's edge words
+            // (this payload's bytes only) after
+            uint64_t sa[kResWords];
+            u32x4 sv[kResWords];
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
                 const uint32_t w = w0 + t + kResBlock * i;
-                if (w >= we) continue;
+                const ResDesc x = s_d[di[i]];
+                const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
+                // no short-circuit: with `&&` the compiler (ROCm 7.2, gfx950)
+                // branched around the descriptor's length and lost the sink
+                // for the last word of a payload on word 0 -- it stored the
+                // whole word, over the next frame's header (r06ap)
+                const bool whole = (w < we) & (a >= x.addr) & (a + 16 <= x.addr + x.len);
+                sa[i] = whole ? a : my_sink;
+                sv[i] = v[i] ^ rot_key(x.key, x.addr);
+            }
+            static_assert(kResWords == 4, "st_sys16x4 stores four words");
+            if (wt) st_sys16x4(sa[0], sv[0], sa[1], sv[1], sa[2], sv[2], sa[3], sv[3]);
+            else st_l2_16x4(sa[0], sv[0], sa[1], sv[1], sa[2], sv[2], sa[3], sv[3]);
+#pragma unroll
+            for (int i = 0; i < kResWords; ++i) {
+                const uint32_t w = w0 + t + kResBlock * i;
                 const ResDesc x = s_d[di[i]];
                 const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
                 const uint64_t end = x.addr + x.len;
+                if (w >= we || (a >= x.addr && a + 16 <= end)) continue;
                 const uint32_t r = rot_key(x.key, x.addr);
-                if (a >= x.addr && a + 16 <= end) {
-                    st_sys16(a, v[i] ^ r);
-                } else {  // a hull's first or last word: this payload's bytes only
-                    const uint64_t lo = a > x.addr ? a : x.addr, hi = a + 16 < end ? a + 16 : end;
-                    for (uint64_t q = lo; q < hi; ++q) {
-                        const uint32_t b = (uint32_t)(q - a);
-                        const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
-                        st_sys1(q, (dw ^ r) >> (8 * (b & 3u)));
-                    }
+                const uint64_t lo = a > x.addr ? a : x.addr, hi = a + 16 < end ? a + 16 : end;
+                for (uint64_t q = lo; q < hi; ++q) {
+                    const uint32_t b = (uint32_t)(q - a);
+                    const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
+                    const uint32_t o = (dw ^ r) >> (8 * (b & 3u));
+                    if (wt) st_sys1(q, o);
+                    else *reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(q) = (uint8_t)o;
                 }
             }
         }
-        // every wave waits for its own stores, then ONE release at system
-        // scope (the L2 written back) with the job number: the host sees every
-        // payload byte before it sees `done`.  A release fence in all 16 waves
-        // cost 2.7 us more per 64 KiB job, 1.2 us per 4 KiB one
-        // (tools/zc_probe.hip, profiles/r05n_zc_probe.jsonl).
+        // every wave waits for its own stores, then ONE lane writes the
+        // part's done word: a small job's stores were written through (in
+        // host memory once vmcnt drains), so no release; a large job's sit in
+        // the L2 and that lane's release writes them back (one release: in all
+        // 16 waves it cost 2.7 us more per 64 KiB job, tools/zc_probe.hip,
+        // profiles/r05n_zc_probe.jsonl)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t == 0) {
+            if (wt) __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else __hip_atomic_store(&sl->done[part], cmd & kJobMask, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (t < 64) {
             last = cmd & kJobMask;
             t_act = wall_clock64();  // the slot was busy until now (a long job is not idle time)

@@ -94,7 +94,9 @@ int main(int argc, char** argv)
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
         th.emplace_back([&, t] {
-            std::vector<uint8_t> a(4096, (uint8_t)t), b;
+            // GI_LEN: bytes per mask (default 4 KiB)
+            const size_t mlen = std::getenv("GI_LEN") ? (size_t)std::strtoul(std::getenv("GI_LEN"), nullptr, 10) : 4096;
+            std::vector<uint8_t> a(mlen, (uint8_t)t), b;
             uint8_t key[4] = {(uint8_t)(t + 1), 0x5A, 0xC3, 0x96};
             if (how == "launch") kmws_resident_enable(0, 0);
             int last_mode = 0;
