@@ -82,6 +82,14 @@ kmws_status kmws_resident_counters(int device, int* thread_slot, int* slots_clai
  * running when its thread exited or switched the worker off). */
 kmws_status kmws_resident_guard_counters(int device, uint64_t* unowned_posts, uint64_t* late_posts,
                                          uint64_t* drained_releases);
+/* Resident jobs posted so far by how their stores reach host memory: written
+ * through (small jobs, and every job while a device batch of this library
+ * runs on the device), or stored into the L2 and released once. */
+kmws_status kmws_resident_store_counters(int device, uint64_t* write_through, uint64_t* released);
+/* 1 while device batches enqueued through this library (kmws_unmask_*,
+ * kmws_unpack_*, kmws_encode_batch, kmws_gather_unmask) are estimated to run
+ * on `device` (20 us + their bytes at 6 TB/s, back to back), else 0. */
+int kmws_device_batch_busy(int device);
 /* Device selection (kmws_gpu.h KMWS_DEVICE_POLICY_*) as a pure function, for
  * tests: the device `policy` gives a thread on NUMA node `thread_node` (-1:
  * unknown) when the GPUs' nodes are gpu_nodes[0..ngpus) and `seq` threads

@@ -100,6 +100,13 @@ kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const Pi
 // KMWS_DEVICE_AUTO -> the calling thread's device (kmws_devmap.cpp; negative
 // without a gfx950 device); any other value unchanged.
 int resolve_device(int device);
+// A device batch (an HBM-resident kernel over `bytes` of traffic) was just
+// enqueued on the calling thread's current device: until about when it should
+// have finished (queued batches add up), the resident grid on that device
+// stores large jobs write-through instead of releasing the L2 once per job
+// (kmws_resident.hip: kResWriteThroughWords).
+void note_device_batch(uint64_t bytes);
+bool device_batch_running(int device);
 
 // Resident worker (kmws_resident.hip): host jobs of at most kResMaxDescs
 // payloads and kResMaxBytes bytes go to the calling thread's slot of a grid

@@ -21,7 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
+#include <atomic>
 #include <cctype>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -189,5 +191,38 @@ kmws_status kmws_device_numa_node(int device, int* node)
 namespace kmws {
 
 int resolve_device(int device) { return device == KMWS_DEVICE_AUTO ? kmws_thread_device() : device; }
+
+// Per device: steady-clock ns until which device batches are assumed to run.
+// An estimate, not a completion signal (an event per batch would cost every
+// resident job a HIP query): 20 us + the batch's bytes at 6 TB/s, queued
+// batches back to back, so a batch on another stream only lengthens it.
+constexpr int kBatchDevices = 64;
+static std::atomic<uint64_t> g_batch_until[kBatchDevices];
+
+static uint64_t steady_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+void note_device_batch(uint64_t bytes)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kBatchDevices) {
+        (void)hipGetLastError();
+        return;
+    }
+    const uint64_t now = steady_ns(), est = 20000u + bytes / 6000u;
+    uint64_t cur = g_batch_until[dev].load(std::memory_order_relaxed);
+    while (!g_batch_until[dev].compare_exchange_weak(cur, (cur > now ? cur : now) + est, std::memory_order_relaxed)) {
+    }
+}
+
+bool device_batch_running(int device)
+{
+    return device >= 0 && device < kBatchDevices &&
+           steady_ns() < g_batch_until[device].load(std::memory_order_relaxed);
+}
 
 }  // namespace kmws

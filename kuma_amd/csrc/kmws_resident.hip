@@ -51,10 +51,13 @@ constexpr int kResBlock = 1024;  // 16 waves: 4 words each = 64 KiB of loads in 
 constexpr int kResWords = 4;
 // Jobs of up to this many 16-byte words store write-through (sc0 sc1) and end
 // without a release; larger ones store into the L2 and end with one
-// system-scope release (a buffer_wbl2 of the XCD's L2).  A release per job at
-// a million small jobs a second slowed a device batch beside the grid
-// (tools/grid_interference.cpp); write-through stores of 64 KiB generations
-// halved 8 loopback connections' decode (18.6 -> 8.6-10.9 GiB/s, r06an-ap).
+// system-scope release (a buffer_wbl2 of the XCD's L2) -- unless a device
+// batch of this library is running on the device (kmws::note_device_batch):
+// then every job writes through.  A release per job at a million small jobs a
+// second slowed a device batch beside the grid (tools/grid_interference.cpp),
+// and with 64 KiB jobs 1.36x against 1.11x written through (r06az); write-
+// through stores of 64 KiB generations halved 8 loopback connections' decode
+// (18.6 -> 8.6-10.9 GiB/s, r06an-ap).  The thread decides (kWriteThroughBit).
 constexpr int kResWriteThroughWords = 1024;
 // Slots per device: one per loop thread that uses the synchronous entries
 // (kuma's test client runs 10 loop threads, its server 5).  Unclaimed slots'
@@ -128,6 +131,7 @@ static_assert(sizeof(ResDesc) == 16, "ResDesc is one 16-byte load");
 // descriptors are then read again after the word.
 constexpr uint64_t kJobMask = (1ull << 40) - 1;
 constexpr int kPartShift = 48;
+constexpr uint64_t kWriteThroughBit = 1ull << 50;  // the job's stores write through (no release)
 constexpr uint64_t kCancelBit = 1ull << 61;
 constexpr uint64_t kClaimedBit = 1ull << 62;
 constexpr uint64_t kQuitBit = 1ull << 63;
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
     __shared__ uint32_t s_pre[kResMaxDescs + 1];  // word prefix over the payload hulls
     __shared__ uint64_t s_cmd;
     __shared__ uint32_t s_have;  // descriptors taken from the poll
-    __shared__ u32x4 s_sink[kResBlock];  // per lane: the words of a lane with none to load or store
+    __shared__ u32x4 s_sink[kResBlock];  // per lane: where a lane with no whole word stores its words
     const int t = threadIdx.x;
     const uint32_t part = blockIdx.x / nslots;
     ResSlot* sl = &mb->slot[(blockIdx.x % nslots + nslots - part % nslots) % nslots];
@@ -413,7 +417,7 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
         }
         __syncthreads();
         const uint32_t total = s_pre[n];
-        const bool wt = total <= (uint32_t)kResWriteThroughWords;  // the same in every part
+        const bool wt = (cmd & kWriteThroughBit) != 0;
         // this part's words: an even share, in job order
         const uint32_t wb = (uint32_t)((uint64_t)total * part / parts), we = (uint32_t)((uint64_t)total * (part + 1) / parts);
         for (uint32_t w0 = wb; w0 < we; w0 += kResBlock * kResWords) {
@@ -422,9 +426,12 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
             uint32_t di[kResWords];
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
-                // a lane past the part's end loads its LDS sink (clamped to the
+                // a lane past the part's end loads nothing (clamped to the
                 // part's last word, many waves reading one host word stalled
-                // the grid: 4 KiB jobs ran at 48 us, r06ao)
+                // the grid: 4 KiB jobs ran at 48 us, r06ao; a load from its
+                // LDS sink instead cost a device batch beside the grid 1.08x
+                // against 1.02x, r06ay).  One asm statement takes every store,
+                // so the compiler's wait for these loads costs nothing more.
                 const uint32_t w = w0 + t + kResBlock * i;
                 uint32_t lo = 0, hi = n;  // last payload whose first word is <= w
                 while (hi - lo > 1) {
@@ -433,8 +440,8 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 }
                 di[i] = lo;
                 const ResDesc x = s_d[lo];
-                const uint64_t a = w < we ? ((x.addr >> 4) + (w - s_pre[lo])) << 4 : my_sink;
-                v[i] = *reinterpret_cast<const u32x4*>(a);  // flat: host memory, or the lane's LDS sink
+                v[i] = u32x4{0, 0, 0, 0};
+                if (w < we) v[i] = *reinterpret_cast<const u32x4*>(((x.addr >> 4) + (w - s_pre[lo])) << 4);
             }
             // whole words first, in one asm statement; a hull's edge words
             // (this payload's bytes only) after
@@ -645,6 +652,8 @@ public:
         uint64_t words = 0;
         for (uint32_t i = 0; i < n; ++i) words += hull_words(d[i].addr, d[i].len);
         const uint32_t parts = (uint32_t)std::min<uint64_t>(kResParts, std::max<uint64_t>(1, words / kPartWords));
+        const bool wt = words <= (uint64_t)kResWriteThroughWords || device_batch_running(device_);
+        __atomic_fetch_add(wt ? &wt_jobs_ : &released_jobs_, 1, __ATOMIC_RELAXED);
         // every polled slot is rewritten, so a stale half always carries job s - 1's tag
         for (uint32_t i = 0; i < n || i < (uint32_t)kPollDescs; ++i) {
             const ResDesc x = tag_desc(i < n ? d[i] : ResDesc{0, 0, 0}, s);
@@ -655,7 +664,9 @@ public:
         __atomic_store_n(&hs_[b].parts, parts, __ATOMIC_RELAXED);
         __atomic_store_n(&hs_[b].seq, s, __ATOMIC_RELEASE);
         __atomic_store_n(&hs_[b].jobs, hs_[b].jobs + 1, __ATOMIC_RELAXED);  // (a withdrawn job is taken off again)
-        __atomic_store_n(&sl.word, s | (uint64_t)n << 40 | (uint64_t)(parts - 1) << kPartShift | kClaimedBit,
+        __atomic_store_n(&sl.word,
+                         s | (uint64_t)n << 40 | (uint64_t)(parts - 1) << kPartShift | (wt ? kWriteThroughBit : 0) |
+                             kClaimedBit,
                          __ATOMIC_RELEASE);
         *job = s;
         return KMWS_OK;
@@ -725,6 +736,8 @@ public:
     uint64_t unowned_posts() const { return ld_acq(&unowned_posts_); }
     uint64_t late_posts() const { return ld_acq(&late_posts_); }
     uint64_t drained() const { return ld_acq(&drained_); }
+    uint64_t wt_jobs() const { return ld_acq(&wt_jobs_); }
+    uint64_t released_jobs() const { return ld_acq(&released_jobs_); }
     int claimed() const { return __builtin_popcount(ld_acq(&claimed_)); }
     // Workgroup exits so far by reason (ResCtl::why), read from device memory.
     kmws_status exit_reasons(uint64_t* out, int n)
@@ -972,6 +985,7 @@ private:
     alignas(64) uint64_t timeouts_ = 0;
     uint64_t withdrawn_ = 0;
     uint64_t unowned_posts_ = 0;  // posts refused: the caller did not hold the slot
+    uint64_t wt_jobs_ = 0, released_jobs_ = 0;  // jobs posted by kind (kWriteThroughBit)
     uint64_t late_posts_ = 0;     // jobs asked for after the thread gave its slots back (launched)
     uint64_t drained_ = 0;        // releases that first waited for the slot's last job
 };
@@ -1176,6 +1190,17 @@ kmws_status kmws_resident_guard_counters(int device, uint64_t* unowned_posts, ui
     if (drained_releases) *drained_releases = w->drained();
     return KMWS_OK;
 }
+
+kmws_status kmws_resident_store_counters(int device, uint64_t* write_through, uint64_t* released)
+{
+    kmws::ResidentWorker* w = kmws::worker(device);
+    if (!w) return KMWS_ERR_INVALID_PARAM;
+    if (write_through) *write_through = w->wt_jobs();
+    if (released) *released = w->released_jobs();
+    return KMWS_OK;
+}
+
+int kmws_device_batch_busy(int device) { return kmws::device_batch_running(device) ? 1 : 0; }
 
 int kmws_thread_attach(int device)
 {

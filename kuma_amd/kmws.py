@@ -53,7 +53,7 @@ BENCH_EXPORTS = [
     "kmws_arena_alloc", "kmws_arena_free", "kmws_arena_place", "kmws_fill_synthetic", "kmws_fill_uniform_descs",
     "kmws_check_unmasked", "kmws_resident_enable", "kmws_resident_info", "kmws_resident_counters",
     "kmws_resident_exit_reasons", "kmws_resident_guard_counters", "kmws_device_policy_pick",
-    "kmws_device_numa_node",
+    "kmws_device_numa_node", "kmws_resident_store_counters", "kmws_device_batch_busy",
 ]
 
 # unmask schedules (include/kmws_gpu.h KMWS_SCHED_*)
@@ -140,6 +140,8 @@ def bind(L: C.CDLL) -> C.CDLL:
         "kmws_resident_enable": (i32, [i32, i32]),
         "kmws_resident_info": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
         "kmws_resident_exit_reasons": (i32, [i32, C.POINTER(C.c_uint64), i32]),
+        "kmws_resident_store_counters": (i32, [i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "kmws_device_batch_busy": (i32, [i32]),
         "kmws_resident_counters": (i32, [i32, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_uint64),
                                          C.POINTER(C.c_uint64)]),
         "kmws_copy_workspace_size": (sz, [u32, u64]),
@@ -369,6 +371,20 @@ def resident_guard(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
     a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
     _check(L.kmws_resident_guard_counters(device, C.byref(a), C.byref(b), C.byref(c)), "kmws_resident_guard_counters")
     return {"unowned_posts": a.value, "late_posts": b.value, "drained_releases": c.value}
+
+
+def resident_stores(device: int = 0, L: Optional[C.CDLL] = None) -> dict:
+    """kmws_resident_store_counters: resident jobs posted that wrote through
+    (small ones, and all while a device batch runs) and that released the L2."""
+    L = L or lib()
+    a, b = C.c_uint64(0), C.c_uint64(0)
+    _check(L.kmws_resident_store_counters(device, C.byref(a), C.byref(b)), "kmws_resident_store_counters")
+    return {"write_through": a.value, "released": b.value}
+
+
+def device_batch_busy(device: int = 0) -> bool:
+    """kmws_device_batch_busy: device batches of this library estimated running."""
+    return lib().kmws_device_batch_busy(device) == 1
 
 
 def device_policy_pick(policy: int, thread_node: int, gpu_nodes: Sequence[int], seq: int) -> int:

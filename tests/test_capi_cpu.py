@@ -209,3 +209,11 @@ def test_copy_workspace_size_follows_the_copy_form():
     above = kmws.copy_workspace_size(n, n * 16384)
     assert above > below + 80 * n // 2
     assert kmws.copy_workspace_size(0, 0) > 0
+
+
+def test_device_batch_busy_without_batches():
+    """kmws_device_batch_busy (no device needed): 0 before any device batch was
+    enqueued, and for devices out of range."""
+    L = kmws.lib()
+    assert [L.kmws_device_batch_busy(d) for d in (0, 1, -1, 64, 1 << 20)] == [0, 0, 0, 0, 0]
+    assert kmws.device_batch_busy(0) is False

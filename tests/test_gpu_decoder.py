@@ -553,6 +553,57 @@ def test_rx_batch_pending_bytes_counts_masked_payloads():
     assert got == want[:4]
 
 
+def test_resident_large_jobs_write_through_while_a_device_batch_runs():
+    """A job above 16 KiB of hull words releases the L2 once on an idle device
+    and writes through while this library's device batches run (kmws_resident.hip
+    kResWriteThroughWords, kmws::note_device_batch); a 4 KiB one always writes
+    through.  Every byte exact, the batch's too."""
+    import time
+    import torch
+    n, frame = 131072, 65536  # 8 GiB: three applies keep the device busy ~8 ms
+    base = torch.empty(n * frame, dtype=torch.uint8, device="cuda")
+    descs = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    kmws.fill_synthetic(base, 7)
+    kmws.fill_uniform_descs(descs, frame, frame, 11)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(base.numel()))
+    kmws.unmask_plan(descs, ws, base.numel())
+    torch.cuda.synchronize()
+    rng = random.Random(77)
+    key = bytes(rng.randrange(256) for _ in range(4))
+
+    def mask(nbytes):
+        data = rng.randbytes(nbytes)
+        buf = bytearray(data)
+        kmws.handle_data_mask(key, [buf])
+        assert bytes(buf) == orc.mask_bytes(key, data)
+
+    t0 = time.monotonic()
+    while kmws.device_batch_busy() and time.monotonic() - t0 < 2:
+        time.sleep(0.001)
+    mask(4096)  # the thread's slot claimed (and the grid sized for it)
+    mask(4096)
+    s0 = kmws.resident_stores()
+    mask(65536)
+    mask(4096)
+    s1 = kmws.resident_stores()
+    assert (s1["released"] - s0["released"], s1["write_through"] - s0["write_through"]) == (1, 1), (s0, s1)
+    for _ in range(3):
+        kmws.unmask_apply(base, descs, ws)
+    assert kmws.device_batch_busy()
+    mask(65536)
+    s2 = kmws.resident_stores()
+    assert (s2["released"] - s1["released"], s2["write_through"] - s1["write_through"]) == (0, 1), (s1, s2)
+    torch.cuda.synchronize()
+    assert kmws.check_unmasked(base, 7, descs) == 0
+    t0 = time.monotonic()
+    while kmws.device_batch_busy() and time.monotonic() - t0 < 2:
+        time.sleep(0.001)
+    assert not kmws.device_batch_busy()
+    mask(65536)
+    s3 = kmws.resident_stores()
+    assert s3["released"] - s2["released"] == 1, (s2, s3)
+
+
 def test_resident_busy_grid_leaves_only_at_its_lease():
     """Four threads masking 4 KiB back to back: over ~30 ms of that (read while
     they still run), every workgroup exit is a lease exit -- none decides the
