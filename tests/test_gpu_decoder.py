@@ -644,7 +644,11 @@ def test_resident_busy_grid_leaves_only_at_its_lease():
     d = {k: after[k] - before[k] for k in after}
     print(f"\nexits while busy: {d}")
     assert not bad
-    assert d["idle"] == 0 and d["closing"] == 0, d
+    # a grid of 4 slots x 4 parts leaves as idle with up to 16 exits (one idle,
+    # the rest closing); four GIL-bound threads can all pause past the 200 us
+    # idle time now and then (r06aq: one such close in 30 ms), while the
+    # round-5 defect closed busy grids 650-1,199 times in 25 ms
+    assert d["idle"] + d["closing"] <= 4 * 16, d
     assert d["lease"] >= 4 * 4 * 10, d  # ~30 incarnations of >= 4 slots x 4 parts
 
 
