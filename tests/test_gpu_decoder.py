@@ -587,12 +587,21 @@ def test_resident_large_jobs_write_through_while_a_device_batch_runs():
     mask(4096)
     s1 = kmws.resident_stores()
     assert (s1["released"] - s0["released"], s1["write_through"] - s0["write_through"]) == (1, 1), (s0, s1)
+    # the boundary: 16 KiB of hull words writes through, one word more releases
+    # (a bytearray's buffer is 16-byte aligned or not; 16 KiB - 15 B fits 1,024
+    # words wherever it lies, 16 KiB + 17 B never does)
+    mask(16384 - 15)
+    mask(16384 + 17)
+    s1b = kmws.resident_stores()
+    assert (s1b["released"] - s1["released"], s1b["write_through"] - s1["write_through"]) == (1, 1), (s1, s1b)
+    s1 = s1b
     for _ in range(3):
         kmws.unmask_apply(base, descs, ws)
     assert kmws.device_batch_busy()
     mask(65536)
+    mask(262144 - 64)  # four parts, written through
     s2 = kmws.resident_stores()
-    assert (s2["released"] - s1["released"], s2["write_through"] - s1["write_through"]) == (0, 1), (s1, s2)
+    assert (s2["released"] - s1["released"], s2["write_through"] - s1["write_through"]) == (0, 2), (s1, s2)
     torch.cuda.synchronize()
     assert kmws.check_unmasked(base, 7, descs) == 0
     t0 = time.monotonic()
