@@ -249,3 +249,47 @@ def test_fuzz_tx_batch(T):
             assert b"".join(bytes(x) for x in segs) == want
 
     print("tx cases:", budget_loop(case))
+
+
+def test_fuzz_mask_chain_both_store_kinds(T):
+    """Random kmws_mask_host_chain calls (1-3 segments, 0 .. 256 KiB, odd
+    offsets) on the resident grid, some right after device batches were
+    enqueued: small jobs and jobs under a running batch write through, large
+    ones on an idle device release the L2 (kmws_resident.hip
+    kResWriteThroughWords); every byte equals the oracle's, the batch's too."""
+    from kuma_amd import kmws
+    n, frame = 16384, 65536  # 1 GiB on the device
+    base = T.empty(n * frame, dtype=T.uint8, device="cuda")
+    descs = T.empty((n, 2), dtype=T.int64, device="cuda")
+    kmws.fill_synthetic(base, 5)
+    kmws.fill_uniform_descs(descs, frame, frame, 9)
+    ws = kmws.Workspace(kmws.unmask_workspace_size(base.numel()))
+    kmws.unmask_plan(descs, ws, base.numel())
+    T.cuda.synchronize()
+    applies = [0]
+    s0 = kmws.resident_stores()
+
+    def case(rng):
+        if rng.random() < 0.3:
+            for _ in range(4):
+                kmws.unmask_apply(base, descs, ws)
+            applies[0] += 4
+        key = bytes(rng.integers(0, 256, size=4, dtype=np.uint8))
+        sizes = [int(rng.choice([0, 1, 15, 4096, 16369, 16401, 65536, 100000])) for _ in range(int(rng.integers(1, 4)))]
+        total = sum(sizes)
+        if total > 262144:
+            sizes = [262144 // len(sizes)] * len(sizes)
+        data = [rng.integers(0, 256, size=s + 17, dtype=np.uint8).tobytes() for s in sizes]
+        offs = [int(rng.integers(0, 17)) for _ in sizes]
+        segs = [bytearray(d[o:o + s]) for d, o, s in zip(data, offs, sizes)]
+        plain = b"".join(bytes(x) for x in segs)
+        kmws.handle_data_mask(key, segs)
+        assert b"".join(bytes(x) for x in segs) == orc.mask_bytes(key, plain)
+
+    print("mask chain cases:", budget_loop(case))
+    if applies[0] % 2 == 0:
+        kmws.unmask_apply(base, descs, ws)
+    T.cuda.synchronize()
+    assert kmws.check_unmasked(base, 5, descs) == 0
+    s1 = kmws.resident_stores()
+    assert s1["write_through"] > s0["write_through"] and s1["released"] > s0["released"], (s0, s1)
