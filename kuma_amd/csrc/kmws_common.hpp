@@ -101,11 +101,12 @@ kmws_status launch_unmask_pieces(uint8_t* base, const kmws_desc* descs, const Pi
 // without a gfx950 device); any other value unchanged.
 int resolve_device(int device);
 // A device batch (an HBM-resident kernel over `bytes` of traffic) was just
-// enqueued on the calling thread's current device: until about when it should
+// enqueued on `stream` (its device; the current device for the null stream):
+// until about when it should
 // have finished (queued batches add up), the resident grid on that device
 // stores large jobs write-through instead of releasing the L2 once per job
 // (kmws_resident.hip: kResWriteThroughWords).
-void note_device_batch(uint64_t bytes);
+void note_device_batch(uint64_t bytes, hipStream_t stream);
 bool device_batch_running(int device);
 
 // Resident worker (kmws_resident.hip): host jobs of at most kResMaxDescs

@@ -206,13 +206,18 @@ static uint64_t steady_ns()
         .count();
 }
 
-void note_device_batch(uint64_t bytes)
+void note_device_batch(uint64_t bytes, hipStream_t stream)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kBatchDevices) {
+    hipDevice_t dev = -1;
+    if (stream && hipStreamGetDevice(stream, &dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
         (void)hipGetLastError();
         return;
     }
+    if (dev < 0 || dev >= kBatchDevices) return;
     const uint64_t now = steady_ns(), est = 20000u + bytes / 6000u;
     uint64_t cur = g_batch_until[dev].load(std::memory_order_relaxed);
     while (!g_batch_until[dev].compare_exchange_weak(cur, (cur > now ? cur : now) + est, std::memory_order_relaxed)) {

@@ -1933,7 +1933,7 @@ kmws_status kmws_encode_batch(const uint8_t* src, const kmws_desc* descs, const 
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    kmws::note_device_batch(2 * dst_cap);
+    kmws::note_device_batch(2 * dst_cap, s);
     return launch_copy<true>(src, dst, dst_cap, wire_off, descs, flags, n, c, s);
 }
 
@@ -1947,7 +1947,7 @@ kmws_status kmws_gather_unmask(const uint8_t* src, const kmws_desc* descs, uint3
         (reinterpret_cast<uintptr_t>(src) & 15u) || !carve(workspace, workspace_bytes, n, dst_cap, c))
         return workspace && workspace_bytes < copy_ws_size(n, dst_cap) ? KMWS_ERR_BUFFER_TOO_SMALL
                                                                        : KMWS_ERR_INVALID_PARAM;
-    kmws::note_device_batch(2 * dst_cap);
+    kmws::note_device_batch(2 * dst_cap, s);
     return launch_copy<false>(src, dst, dst_cap, dst_off, descs, nullptr, n, c, s);
 }
 
@@ -1968,7 +1968,7 @@ kmws_status kmws_unpack_gather(const uint8_t* wire, uint64_t wire_len, const uin
                                                                        : KMWS_ERR_INVALID_PARAM;
     if (launch_zero(c.head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     if (n == 0) return launch_zero(dst_off, sizeof(uint64_t), s);
-    kmws::note_device_batch(wire_len + dst_cap);
+    kmws::note_device_batch(wire_len + dst_cap, s);
     kmws_status st = launch_reduce(HeaderPayloadSize{wire, wire_len, hdr_off, n, mode, out_desc, out_flags, out_err,
                                                      c.head},
                                    n, dst_off, c, s);

@@ -701,7 +701,7 @@ kmws_status kmws_unmask_apply_sched(uint8_t* base, uint64_t span, const kmws_des
 {
     if (bad_args(base, descs, n, workspace)) return KMWS_ERR_INVALID_PARAM;
     const uint32_t code = schedule < 0 ? default_schedule(span, n) : (uint32_t)schedule;
-    kmws::note_device_batch(2 * span);
+    kmws::note_device_batch(2 * span, static_cast<hipStream_t>(stream));
     return launch_apply(code, base, span, descs, n, workspace, workspace_bytes, static_cast<hipStream_t>(stream));
 }
 
@@ -723,7 +723,7 @@ kmws_status kmws_unpack_unmask(uint8_t* wire, uint64_t wire_len, const uint64_t*
     WsHead* head = static_cast<WsHead*>(workspace);
     if (launch_zero(head, sizeof(WsHead), s) != KMWS_OK) return KMWS_ERR_FAILED;
     if (n == 0) return KMWS_OK;
-    kmws::note_device_batch(2 * wire_len);
+    kmws::note_device_batch(2 * wire_len, s);
     hipLaunchKernelGGL(unpack_plan_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, wire, wire_len, hdr_off,
                        n, mode, out_desc, out_flags, out_err, ilog2_u64(ProdCfg::kTile),
                        reinterpret_cast<uint32_t*>(head + 1), head);
