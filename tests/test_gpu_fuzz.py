@@ -291,5 +291,19 @@ def test_fuzz_mask_chain_both_store_kinds(T):
         kmws.unmask_apply(base, descs, ws)
     T.cuda.synchronize()
     assert kmws.check_unmasked(base, 5, descs) == 0
+    # the batches above were queued faster than they ran, so the device may
+    # have been busy throughout (every job written through); once the estimate
+    # runs out (it adds up per batch, so it can trail the real end by a second
+    # after 8 s of them), large jobs release
+    t_end = time.time() + 5
+    while kmws.device_batch_busy() and time.time() < t_end:
+        time.sleep(0.005)
+    assert not kmws.device_batch_busy()
+    rng = np.random.default_rng(1)
+    for _ in range(3):
+        seg = bytearray(rng.integers(0, 256, size=65536, dtype=np.uint8).tobytes())
+        want = orc.mask_bytes(b"\x01\x02\x03\x04", bytes(seg))
+        kmws.handle_data_mask(b"\x01\x02\x03\x04", [seg])
+        assert bytes(seg) == want
     s1 = kmws.resident_stores()
     assert s1["write_through"] > s0["write_through"] and s1["released"] > s0["released"], (s0, s1)
