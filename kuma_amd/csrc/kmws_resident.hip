@@ -222,22 +222,8 @@ __device__ __forceinline__ void st_sys16x4(uint64_t a0, u32x4 v0, uint64_t a1, u
         "v"(v0), "v"(a1), "v"(v1), "v"(a2), "v"(v2), "v"(a3), "v"(v3)
         : "memory");
 }
-// The same four words into the L2 (write-back): a large job's stores, made
-// visible by one release at its end (see kResWriteThroughWords).
-__device__ __forceinline__ void st_l2_16x4(uint64_t a0, u32x4 v0, uint64_t a1, u32x4 v1, uint64_t a2, u32x4 v2,
-                                           uint64_t a3, u32x4 v3)
-{
-    asm volatile(
-        "flat_store_dwordx4 %0, %1\n\t"
-        "flat_store_dwordx4 %2, %3\n\t"
-        "flat_store_dwordx4 %4, %5\n\t"
-        "flat_store_dwordx4 %6, %7\n\t"
-        "s_nop 1" ::"v"(a0),
-        "v"(v0), "v"(a1), "v"(v1), "v"(a2), "v"(v2), "v"(a3), "v"(v3)
-        : "memory");
-}
 // A small job's hull edge bytes, written through: stores the compiler counts
-// (no wait between them); a large job's edge bytes are plain stores.
+// (no wait between them).
 __device__ __forceinline__ void st_sys1(uint64_t a, uint32_t v)
 {
     __hip_atomic_store(reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(a), (uint8_t)v, __ATOMIC_RELAXED,
@@ -443,41 +429,46 @@ __global__ void __launch_bounds__(kResBlock) resident_unmask_kernel(ResMailbox* 
                 v[i] = u32x4{0, 0, 0, 0};
                 if (w < we) v[i] = *reinterpret_cast<const u32x4*>(((x.addr >> 4) + (w - s_pre[lo])) << 4);
             }
-            // whole words first, in one asm statement; a hull's edge words
-            // (this payload's bytes only) after
-            uint64_t sa[kResWords];
+            // each word XORed with its payload's rotated key (the loads' registers
+            // free from here: fewer live VGPRs leave more of each SIMD to a device
+            // batch sharing the CU -- 96 against 82 cost that batch 1.07-1.08x
+            // against 1.02x, r06bq)
             u32x4 sv[kResWords];
+            uint64_t sa[kResWords];
+            uint32_t edge = 0;  // bit i: word i is a hull's edge word of this part
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
                 const uint32_t w = w0 + t + kResBlock * i;
                 const ResDesc x = s_d[di[i]];
                 const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
+                sv[i] = v[i] ^ rot_key(x.key, x.addr);
+                sa[i] = a;
                 // no short-circuit: with `&&` the compiler (ROCm 7.2, gfx950)
                 // branched around the descriptor's length and lost the sink
                 // for the last word of a payload on word 0 -- it stored the
                 // whole word, over the next frame's header (r06ap)
-                const bool whole = (w < we) & (a >= x.addr) & (a + 16 <= x.addr + x.len);
-                sa[i] = whole ? a : my_sink;
-                sv[i] = v[i] ^ rot_key(x.key, x.addr);
+                const bool in = w < we, whole = in & (a >= x.addr) & (a + 16 <= x.addr + x.len);
+                edge |= (uint32_t)(in & !whole) << i;
+                if (wt) sa[i] = whole ? a : my_sink;
+                else if (whole) *reinterpret_cast<u32x4*>(a) = sv[i];  // into the L2 (the release follows)
             }
+            // write-through: the four words in one asm statement
             static_assert(kResWords == 4, "st_sys16x4 stores four words");
             if (wt) st_sys16x4(sa[0], sv[0], sa[1], sv[1], sa[2], sv[2], sa[3], sv[3]);
-            else st_l2_16x4(sa[0], sv[0], sa[1], sv[1], sa[2], sv[2], sa[3], sv[3]);
+            // a hull's edge words: this payload's bytes only
 #pragma unroll
             for (int i = 0; i < kResWords; ++i) {
-                const uint32_t w = w0 + t + kResBlock * i;
+                if (!(edge >> i & 1u)) continue;
                 const ResDesc x = s_d[di[i]];
-                const uint64_t a = ((x.addr >> 4) + (w - s_pre[di[i]])) << 4;
+                const uint64_t a = sa[i] == my_sink ? ((x.addr >> 4) + (w0 + t + kResBlock * i - s_pre[di[i]])) << 4 : sa[i];
                 const uint64_t end = x.addr + x.len;
-                if (w >= we || (a >= x.addr && a + 16 <= end)) continue;
-                const uint32_t r = rot_key(x.key, x.addr);
                 const uint64_t lo = a > x.addr ? a : x.addr, hi = a + 16 < end ? a + 16 : end;
                 for (uint64_t q = lo; q < hi; ++q) {
                     const uint32_t b = (uint32_t)(q - a);
-                    const uint32_t dw = (b & 8u) ? ((b & 4u) ? v[i].w : v[i].z) : ((b & 4u) ? v[i].y : v[i].x);
-                    const uint32_t o = (dw ^ r) >> (8 * (b & 3u));
+                    const uint32_t dw = (b & 8u) ? ((b & 4u) ? sv[i].w : sv[i].z) : ((b & 4u) ? sv[i].y : sv[i].x);
+                    const uint32_t o = dw >> (8 * (b & 3u));
                     if (wt) st_sys1(q, o);
-                    else *reinterpret_cast<__attribute__((address_space(1))) uint8_t*>(q) = (uint8_t)o;
+                    else *reinterpret_cast<uint8_t*>(q) = (uint8_t)o;
                 }
             }
         }
